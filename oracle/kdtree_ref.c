@@ -1,0 +1,259 @@
+/*
+ * kdtree_ref.c -- oracle restatement of the reference KD-tree build and its
+ * BFS flatten.  TEST INFRASTRUCTURE ONLY (see mcpt_oracle.h).
+ *
+ * Build: QE/Utils/KDTree.hpp:58-287
+ *   - FIFO work list from the root (all triangles, AABB = union of tri AABBs);
+ *   - depth >= 32 -> leaf (:103-106);
+ *   - > 64 triangles: spatial median of the longest axis (strict '>' picks
+ *     the first longest), value 0.5f*(max+min) (:108-122);
+ *   - <= 64: SAH over every vertex coordinate per axis, candidates in
+ *     std::set<KDSplit> order (axis, value; first-inserted kept on ties),
+ *     SAH = (AL*nL + AR*nR)/A0 + 0, first strict minimum wins, split only if
+ *     minSAH < N (:164-285).  Empty-side candidates evaluate to NaN and never win;
+ *   - triangle classification: flat-on-plane -> left; min < v -> left,
+ *     max > v -> right (:129-153);
+ *   - child AABB = parent AABB cut at v, intersected with the union of its
+ *     triangles' AABBs (QuinAABB::operator*=, Structure.hpp:133-141).
+ *   std::min/std::max are reproduced literally ((b<a)?b:a / (a<b)?b:a).
+ * Flatten: QE/RTX/ShaderResource.hpp:128-179 -- BFS order; the children of a
+ *   node are consecutive (left = BFS index, right = left+1); leaf triangle ids
+ *   ascending (std::set<UINT>).  Leaves keep all ids (no 64-slot cap).
+ */
+#include "oracle_internal.h"
+
+#include <float.h>
+#include <stdlib.h>
+#include <string.h>
+
+typedef struct { float mn[3], mx[3]; } aabb_t;
+
+static inline float smin(float a, float b) { return (b < a) ? b : a; }   /* std::min */
+static inline float smax(float a, float b) { return (a < b) ? b : a; }   /* std::max */
+
+static void aabb_empty(aabb_t* b) {          /* QuinAABB(false) / Clear() */
+    for (int i = 0; i < 3; i++) { b->mn[i] = FLT_MAX; b->mx[i] = -FLT_MAX; }
+}
+static void aabb_add_pt(aabb_t* b, const float* p) {   /* QuinAABB::Add */
+    for (int i = 0; i < 3; i++) { b->mn[i] = smin(b->mn[i], p[i]); b->mx[i] = smax(b->mx[i], p[i]); }
+}
+static void aabb_add(aabb_t* b, const aabb_t* r) {     /* operator+= */
+    aabb_add_pt(b, r->mn);
+    aabb_add_pt(b, r->mx);
+}
+static void aabb_clip(aabb_t* b, const aabb_t* r) {    /* operator*= */
+    for (int i = 0; i < 3; i++) { b->mn[i] = smax(b->mn[i], r->mn[i]); b->mx[i] = smin(b->mx[i], r->mx[i]); }
+}
+
+typedef struct {
+    aabb_t box;
+    uint32_t axis;   /* 0 none */
+    float split;
+    int left, right;
+    int* ids; int nids;
+    int depth;
+} bnode;
+
+typedef struct {
+    const float (*v)[3][3];   /* kd tri -> 3 vertices */
+    const aabb_t* tbox;
+} ctx_t;
+
+static aabb_t node_aabb(const ctx_t* c, const int* ids, int n) {   /* GetNodeAABB */
+    aabb_t b;
+    aabb_empty(&b);
+    for (int i = 0; i < n; i++) aabb_add(&b, &c->tbox[ids[i]]);
+    return b;
+}
+
+typedef struct { float v; int ins; } cand_t;
+static int cand_cmp(const void* a, const void* b) {
+    const cand_t* x = (const cand_t*)a;
+    const cand_t* y = (const cand_t*)b;
+    if (x->v < y->v) return -1;
+    if (y->v < x->v) return 1;
+    return (x->ins > y->ins) - (x->ins < y->ins);
+}
+
+/* split node's ids by (axis, v) into two new arrays */
+static void classify(const ctx_t* c, const int* ids, int n, int ax, float v,
+                     int** L, int* nL, int** R, int* nR) {
+    *L = (int*)malloc(sizeof(int) * (size_t)(n ? n : 1));
+    *R = (int*)malloc(sizeof(int) * (size_t)(n ? n : 1));
+    *nL = *nR = 0;
+    for (int i = 0; i < n; i++) {
+        const aabb_t* tb = &c->tbox[ids[i]];
+        if (tb->mn[ax] == tb->mx[ax] && tb->mn[ax] == v) {
+            (*L)[(*nL)++] = ids[i];
+        } else {
+            if (tb->mn[ax] < v) (*L)[(*nL)++] = ids[i];
+            if (tb->mx[ax] > v) (*R)[(*nR)++] = ids[i];
+        }
+    }
+}
+
+void orc_kd_build(orc_scene* s) {
+    const orc_model* m = &s->model;
+    int n = s->nkd;
+    float (*tv)[3][3] = malloc(sizeof(float[3][3]) * (size_t)(n ? n : 1));
+    aabb_t* tbox = malloc(sizeof(aabb_t) * (size_t)(n ? n : 1));
+    for (int k = 0; k < n; k++) {
+        const orc_tri* t = &m->tris[s->kd_tris[k]];
+        for (int j = 0; j < 3; j++) {
+            const orc_v3* p = &m->verts[t->v[j]];
+            tv[k][j][0] = p->x; tv[k][j][1] = p->y; tv[k][j][2] = p->z;
+        }
+        aabb_empty(&tbox[k]);
+        for (int j = 0; j < 3; j++) aabb_add_pt(&tbox[k], tv[k][j]);
+    }
+    ctx_t c = {(const float(*)[3][3])tv, tbox};
+
+    int cap = 1024, nn = 0;
+    bnode* nodes = malloc(sizeof(bnode) * (size_t)cap);
+    int* queue = malloc(sizeof(int) * (size_t)cap);
+    int qh = 0, qt = 0, qcap = cap;
+
+    bnode root;
+    memset(&root, 0, sizeof root);
+    root.ids = malloc(sizeof(int) * (size_t)(n ? n : 1));
+    root.nids = n;
+    for (int i = 0; i < n; i++) root.ids[i] = i;
+    root.box = node_aabb(&c, root.ids, n);
+    root.left = root.right = -1;
+    nodes[nn++] = root;
+    queue[qt++] = 0;
+    int maxdepth = 0;
+
+    while (qh < qt) {
+        int ni = queue[qh++];
+        int depth = nodes[ni].depth;
+        if (depth > maxdepth) maxdepth = depth;
+        if (depth >= 32) continue;
+        bnode nd = nodes[ni];
+        int ax = -1;
+        float val = 0.0f;
+        if (nd.nids > 64) {
+            float sz[3];
+            for (int i = 0; i < 3; i++) sz[i] = nd.box.mx[i] - nd.box.mn[i];
+            float best = sz[0];
+            ax = 0;
+            for (int i = 1; i < 3; i++) if (sz[i] > best) { best = sz[i]; ax = i; }
+            val = 0.5f * (nd.box.mx[ax] + nd.box.mn[ax]);
+        } else {
+            float sz[3];
+            for (int i = 0; i < 3; i++) sz[i] = nd.box.mx[i] - nd.box.mn[i];
+            float A0 = sz[0] * sz[1] + sz[1] * sz[2] + sz[2] * sz[0];
+            float SAH0 = (float)(unsigned)nd.nids;
+            float minSAH = FLT_MAX;
+            int min_ax = -1;
+            float min_v = 0.0f;
+            cand_t* cands = malloc(sizeof(cand_t) * (size_t)(3 * nd.nids + 1));
+            for (int a = 0; a < 3; a++) {
+                int nc = 0;
+                for (int i = 0; i < nd.nids; i++)
+                    for (int j = 0; j < 3; j++) { cands[nc].v = tv[nd.ids[i]][j][a]; cands[nc].ins = nc; nc++; }
+                qsort(cands, (size_t)nc, sizeof(cand_t), cand_cmp);
+                for (int q = 0; q < nc; q++) {
+                    if (q > 0 && !(cands[q - 1].v < cands[q].v)) continue;   /* set: keep first of equals */
+                    float v = cands[q].v;
+                    if (v < nd.box.mn[a] || v > nd.box.mx[a]) continue;
+                    unsigned numL = 0, numR = 0;
+                    aabb_t bL = nd.box, bR = nd.box, bLt, bRt;
+                    bL.mx[a] = v;
+                    bR.mn[a] = v;
+                    aabb_empty(&bLt);
+                    aabb_empty(&bRt);
+                    for (int i = 0; i < nd.nids; i++) {
+                        const aabb_t* tb = &tbox[nd.ids[i]];
+                        if (tb->mn[a] == tb->mx[a] && tb->mn[a] == v) {
+                            ++numL; aabb_add(&bLt, tb);
+                        } else {
+                            if (tb->mn[a] < v) { ++numL; aabb_add(&bLt, tb); }
+                            if (tb->mx[a] > v) { ++numR; aabb_add(&bRt, tb); }
+                        }
+                    }
+                    aabb_clip(&bL, &bLt);
+                    aabb_clip(&bR, &bRt);
+                    float sL[3], sR[3];
+                    for (int i = 0; i < 3; i++) { sL[i] = bL.mx[i] - bL.mn[i]; sR[i] = bR.mx[i] - bR.mn[i]; }
+                    float AL = sL[0] * sL[1] + sL[1] * sL[2] + sL[2] * sL[0];
+                    float AR = sR[0] * sR[1] + sR[1] * sR[2] + sR[2] * sR[0];
+                    float SAH = (AL * (float)numL + AR * (float)numR) / A0 + 0.0f;
+                    if (SAH < minSAH) { minSAH = SAH; min_ax = a; min_v = v; }
+                }
+            }
+            free(cands);
+            if (minSAH < SAH0) { ax = min_ax; val = min_v; }
+        }
+        if (ax < 0) continue;   /* leaf */
+
+        int *L, *R, nL, nR;
+        classify(&c, nd.ids, nd.nids, ax, val, &L, &nL, &R, &nR);
+        if (nn + 2 > cap) {
+            cap *= 2;
+            nodes = realloc(nodes, sizeof(bnode) * (size_t)cap);
+        }
+        if (qt + 2 > qcap) {
+            qcap *= 2;
+            queue = realloc(queue, sizeof(int) * (size_t)qcap);
+        }
+        bnode l, r;
+        memset(&l, 0, sizeof l);
+        memset(&r, 0, sizeof r);
+        l.box = nd.box; l.box.mx[ax] = val;
+        r.box = nd.box; r.box.mn[ax] = val;
+        aabb_t tl = node_aabb(&c, L, nL), tr = node_aabb(&c, R, nR);
+        aabb_clip(&l.box, &tl);
+        aabb_clip(&r.box, &tr);
+        l.ids = L; l.nids = nL; l.depth = depth + 1; l.left = l.right = -1;
+        r.ids = R; r.nids = nR; r.depth = depth + 1; r.left = r.right = -1;
+        nodes[ni].axis = (uint32_t)(ax + 1);
+        nodes[ni].split = val;
+        nodes[ni].left = nn;
+        nodes[ni].right = nn + 1;
+        free(nodes[ni].ids);
+        nodes[ni].ids = NULL;
+        nodes[ni].nids = 0;
+        nodes[nn++] = l;
+        nodes[nn++] = r;
+        queue[qt++] = nn - 2;
+        queue[qt++] = nn - 1;
+    }
+
+    /* BFS flatten (ShaderResource.hpp:128-179) */
+    s->nodes = malloc(sizeof(orc_node) * (size_t)nn);
+    int nleaf = 0;
+    for (int i = 0; i < nn; i++) nleaf += nodes[i].nids;
+    s->leaf_ids = malloc(sizeof(uint32_t) * (size_t)(nleaf ? nleaf : 1));
+    int* bfs = malloc(sizeof(int) * (size_t)nn);
+    int bh = 0, bt = 0, out = 0, lo = 0;
+    bfs[bt++] = 0;
+    while (bh < bt) {
+        int ni = bfs[bh++];
+        const bnode* b = &nodes[ni];
+        orc_node* o = &s->nodes[out];
+        memset(o, 0, sizeof *o);
+        for (int i = 0; i < 3; i++) { o->bmin[i] = b->box.mn[i]; o->bmax[i] = b->box.mx[i]; }
+        if (b->axis != 0) {
+            o->left = (uint32_t)((bt - bh) + out + 1);
+            o->right = (uint32_t)((bt - bh) + out + 2);
+            o->axis = b->axis;
+            o->split = b->split;
+            bfs[bt++] = b->left;
+            bfs[bt++] = b->right;
+        } else {
+            o->left = o->right = 0xFFFFFFFFu;
+            o->axis = 0;
+            o->split = 0.0f;
+            o->tri_begin = (uint32_t)lo;
+            o->tri_count = (uint32_t)b->nids;
+            for (int i = 0; i < b->nids; i++) s->leaf_ids[lo++] = (uint32_t)b->ids[i];
+        }
+        out++;
+    }
+    s->nnodes = nn;
+    s->nleaf_ids = nleaf;
+    s->kd_depth = maxdepth;
+    for (int i = 0; i < nn; i++) free(nodes[i].ids);
+    free(nodes); free(queue); free(bfs); free(tv); free(tbox);
+}

@@ -1,0 +1,129 @@
+/*
+ * mcpt_oracle.h -- CPU oracle for the Monte Carlo path-tracing hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load this library, and only as the
+ * checker / CPU reference timing.  The product (montecarlopathtracer_amd)
+ * never links, loads or calls it.
+ *
+ * What it restates (reference = pw1316/MonteCarloPathTracer, read-only):
+ *   CV/ = CVMCTracer/CVMCTracer/,  QE/ = MCRT/QuinEngine/
+ *   - OBJ/MTL loader            CV/Framework/ObjReader.cpp:8-259, ObjReader.hpp:37-139
+ *   - geometry upload semantics CV/CUDA/CUTracer.cu:225-314 (groups in std::map order,
+ *                               material of the group's first triangle)
+ *   - KD-tree build             QE/Utils/KDTree.hpp:58-287 (median >64, SAH <=64, depth 32)
+ *   - KD BFS flatten            QE/RTX/ShaderResource.hpp:128-179
+ *   - closest hit, brute force  CV/CUDA/CUTracer.cu:44-96 with Math.hpp:169-175 det()
+ *   - closest hit, KD (ref)     QE/Shader/rtx.hlsl:84-211 (stack DFS, AABB slab test)
+ *   - samplers                  CV/CUDA/Utils.hpp:46-137
+ *   - path loop                 CV/CUDA/CUTracer.cu:98-177
+ *   - primary ray + accumulate  CV/CUDA/CUTracer.cu:179-218, camera :347-374
+ *
+ * Where the reference is not reproducible, the build's own specification is
+ * used (DESIGN.md "Determinism spec"):
+ *   - RNG: cuRAND XORWOW seeded from std::random_device (CUTracer.cu:186-187,
+ *     :375-376) cannot be reproduced; we use the reference's other generator,
+ *     TEA-16 seeding + Park-Miller/Schrage (QE/Shader/rtx.hlsl:61-82), keyed
+ *     statelessly per (pixel, sample).
+ *   - sinf/cosf/powf: device libm differs from glibc by ulps; both sides use
+ *     the fixed double-precision sequences in this file (mc_sin_d etc.).
+ *   - KD "ordered" mode (traversal == 2): the exact traversal order the HIP
+ *     kernel uses, so node/triangle counts and tie-breaks are comparable
+ *     bit for bit.  Its closest hit equals brute force except on exact t ties.
+ *
+ * Parity pinning: the reference's C++ sources need Windows/D3DX/CUDA headers
+ * (stdafx.h) and are unbuildable here; only the vendored tinyobjloader v1.1.1
+ * header builds (oracle/ref/).  The loader is pinned against it; the renderer
+ * is pinned statistically against the reference's own renders
+ * (CV/result1.png and the result1step PNG series) -- see DESIGN.md.
+ */
+#ifndef MCPT_ORACLE_H
+#define MCPT_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct orc_scene orc_scene;
+
+typedef struct {
+    int32_t width, height;          /* full image size (pixel index = y*W + x) */
+    int32_t x0, y0, x1, y1;         /* region to render, [x0,x1) x [y0,y1)      */
+    uint32_t spp;                   /* samples this call                         */
+    uint32_t spp_offset;            /* first global sample index                 */
+    uint32_t spp_chunk;             /* summation chunk (0 = spp)                 */
+    int32_t max_depth;              /* scatter events (reference literal 7)      */
+    float illum;                    /* emitter scale (reference ILLUM 10)        */
+    float tan_half_fov;             /* tan(fov/2) as float                       */
+    float eye[3], fwd[3], up[3], right[3];
+    uint64_t seed;
+    int32_t traversal;              /* 0 brute, 1 reference KD, 2 ordered KD     */
+    int32_t threads;                /* <=0: 1                                    */
+    uint32_t prev_count;            /* running-mean count (CUTracer.cu:215-217)  */
+    int32_t fresnel_kd;             /* 1: color *= Kd on Fresnel (CUTracer.cu:131-133);
+                                       0: no tint (rtx.hlsl:345, the published renders) */
+} orc_params;
+
+typedef struct {
+    uint64_t rays;          /* closest-hit queries                  */
+    uint64_t paths;
+    uint64_t inner_visits;  /* inner KD nodes visited               */
+    uint64_t leaf_visits;   /* leaves visited                       */
+    uint64_t leaf_refs;     /* leaf triangle references read        */
+    uint64_t tri_tests;     /* ray/triangle tests                   */
+    uint64_t shades;        /* non-terminal hits shaded             */
+    uint64_t stack_max;     /* deepest traversal stack (ordered)    */
+} orc_counters;
+
+/* scene ------------------------------------------------------------------ */
+orc_scene* orc_scene_load(const char* obj_path, char* err, int errlen);
+void orc_scene_free(orc_scene* s);
+/* info[0..9] = nverts, nnormals, ntris(incl. dummy), nmats, ngroups,
+ *              ngeoms, nkd_tris, nnodes, nleaf_ids, kd_depth              */
+void orc_scene_info(const orc_scene* s, int64_t* info);
+void orc_copy_vertices(const orc_scene* s, float* out);          /* nverts*3   */
+void orc_copy_normals(const orc_scene* s, float* out);           /* nnormals*3 */
+void orc_copy_triangles(const orc_scene* s, int32_t* out);       /* ntris*10: v3 t3 n3 mat */
+void orc_copy_materials(const orc_scene* s, double* out);        /* nmats*12: Ka Kd Ks Ns Tr Ni */
+/* groups: name of group g (sorted) and its triangle index list */
+const char* orc_group_name(const orc_scene* s, int g);
+int orc_group_ntris(const orc_scene* s, int g);
+void orc_group_tris(const orc_scene* s, int g, int32_t* out);
+void orc_copy_geoms(const orc_scene* s, float* out);             /* ngeoms*14: Ka Kd Ks Ns Tr Ni start count */
+void orc_copy_kd_tris(const orc_scene* s, int32_t* out);         /* kd id -> CV triangle index */
+/* nodes: nnodes*10 floats-as-words: left right axis split(bits) min3 max3 ; leaf ranges separately */
+void orc_copy_kd_nodes(const orc_scene* s, uint32_t* out);       /* nnodes*12 words */
+void orc_copy_kd_leaf_ids(const orc_scene* s, uint32_t* out);
+
+/* building blocks for known-answer tests ---------------------------------- */
+float orc_det3(const float* m9);                                 /* Math.hpp:169-175 */
+uint32_t orc_tea16(uint32_t v0, uint32_t v1);
+uint32_t orc_rng_init(uint32_t pixel, uint32_t key, uint32_t sample);
+float orc_rng_next(uint32_t* state);
+uint32_t orc_seed_key(uint64_t seed);
+float orc_sinf(float x);
+float orc_cosf(float x);
+float orc_powf(float x, float y);
+/* samplers with injected uniforms: u = uniforms consumed in order */
+void orc_sample_hemi(const float* n, const float* u, float* out);
+void orc_sample_phong(const float* n, const float* in, uint32_t Ns, const float* u, float* out);
+void orc_sample_fresnel(const float* n, const float* in, float Tr, float Ni, const float* u, float* out);
+float orc_tan_half_fov(float fov_deg);
+void orc_camera_basis(const float* eye, const float* dir, const float* up,
+                      float* fwd_out, float* up_out, float* right_out);
+
+/* closest hit for a batch of rays: tri_out = kd id (-1 miss),
+ * geom_out = geometry index, hit_out = beta gamma t hx hy hz              */
+void orc_intersect_batch(const orc_scene* s, int traversal, int64_t n,
+                         const float* o, const float* d, int32_t* tri_out,
+                         int32_t* geom_out, float* hit_out, orc_counters* c);
+
+/* render region; out is W*H*3 floats (only region written); if prev_count>0
+ * out holds the previous running mean and is updated in place            */
+int orc_render(const orc_scene* s, const orc_params* p, float* out, orc_counters* c);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
