@@ -1,0 +1,167 @@
+/*
+ * mcpt.h -- C ABI of the MI355X Monte Carlo path-tracing core (libmcpt.so).
+ *
+ * Drop-in boundary for the reference's tracer module, pw1316/MonteCarloPathTracer
+ * CVMCTracer/CVMCTracer/CUDA/CUTracer.h:9-12 (namespace PW::Tracer), whose only
+ * caller is CVMCTracer/CVMCTracer/main.cpp:16-18,33-35.  Plain C types only:
+ * no HIP, torch or C++ types cross this boundary.  Every function returns
+ * MCPT_OK (0) or a negative MCPT_E* code; mcpt_last_error() gives a
+ * thread-local message for the last failure on the calling thread.
+ *
+ *   reference                                         this ABI
+ *   ObjModel::readObj(path)  ObjReader.cpp:8-161      mcpt_model_read_obj
+ *   cudaError_t Initialize() CUTracer.cu:220-223      mcpt_init
+ *   cudaError_t CreateGeometry(const ObjModel*)       mcpt_scene_create (+ KD build,
+ *                            CUTracer.cu:225-314       QuinEngine/Utils/KDTree.hpp:58-287)
+ *   cudaError_t DestroyGeometry() CUTracer.cu:316-338 mcpt_scene_destroy (frees what it allocated)
+ *   cudaError_t RenderScene(int sceneID, PWVector3f*) mcpt_render (host framebuffer, synchronous)
+ *                            CUTracer.cu:340-404       mcpt_render_device (device buffer, async)
+ *
+ * Ownership: a model/scene handle is owned by the caller and used from one
+ * thread at a time; the scene owns its device copies; framebuffers are
+ * caller-owned.  Framebuffer layout = the reference's hostcolor: row-major
+ * y*W + x, linear radiance, fp32 RGB (3 floats per pixel) for mcpt_render;
+ * RGBA (4 floats per pixel, A unused) for mcpt_render_device.
+ */
+#ifndef MCPT_H
+#define MCPT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MCPT_ABI_VERSION 1
+
+enum {
+    MCPT_OK = 0,
+    MCPT_E_INVALID = -1,   /* bad argument                     */
+    MCPT_E_IO = -2,        /* file cannot be opened            */
+    MCPT_E_PARSE = -3,     /* "Invalid OBJ file!" (ObjReader.cpp:81) */
+    MCPT_E_DEVICE = -4,    /* HIP runtime error                */
+    MCPT_E_NOMEM = -5,
+    MCPT_E_UNSUPPORTED = -6
+};
+
+typedef struct mcpt_model mcpt_model;   /* host ObjModel (ObjReader.hpp:37-63)  */
+typedef struct mcpt_scene mcpt_scene;   /* device-resident scene + KD tree      */
+
+typedef struct {
+    int64_t n_vertices;    /* incl. dummy index 0 (ObjReader.hpp:44) */
+    int64_t n_normals;     /* incl. dummy */
+    int64_t n_texcoords;   /* incl. dummy */
+    int64_t n_triangles;   /* incl. dummy */
+    int64_t n_materials;   /* incl. dummy "" material */
+    int64_t n_groups;      /* incl. empty ones, std::map order */
+} mcpt_model_info;
+
+typedef struct {
+    int64_t n_geometries;  /* non-empty groups (CUTracer.cu:278-285) */
+    int64_t n_triangles;   /* triangles covered by a geometry range (KD input) */
+    int64_t n_nodes;       /* KD nodes, BFS order */
+    int64_t n_leaf_refs;   /* total leaf triangle references */
+    int64_t kd_depth;      /* deepest node depth (<= 32) */
+    int64_t lds_bytes;     /* LDS image size; 0 if the scene is served from global memory */
+    int64_t device;        /* HIP device ordinal holding the scene */
+} mcpt_scene_info;
+
+typedef struct {
+    int32_t width, height;      /* full image (IMG_WIDTH/IMG_HEIGHT, CV/stdafx.h:41-42) */
+    uint32_t spp;               /* samples per pixel this call (NUM_SAMPLES_PER_KERNEL) */
+    uint32_t spp_offset;        /* first global sample index (progressive / sharded spp) */
+    uint32_t spp_chunk;         /* samples summed per partial, 0 = spp (summation order) */
+    int32_t max_depth;          /* scatter events, reference literal 7 (CUTracer.cu:212) */
+    float illum;                /* emitter scale, ILLUM 10 (CV/stdafx.h:45) */
+    float fov_deg;              /* horizontal FOV, 60 (CUTracer.cu:189) */
+    float eye[3], dir[3], up[3];/* camera lookAt (CUTracer.cu:349-355) */
+    uint64_t seed;              /* RNG seed (DESIGN.md determinism spec) */
+    uint32_t prev_count;        /* running mean: fb = (fb*prev + mean)/(prev+1) (CUTracer.cu:215-217) */
+    int32_t fresnel_kd;         /* 1: Fresnel multiplies Kd (CUTracer.cu:131-133); 0: not (rtx.hlsl:345) */
+    int32_t tile;               /* pixel tile edge for sharding/ordering, 0 = 8 */
+    int32_t shard_count;        /* tiles t with t % shard_count == shard_index are rendered; 0/1 = all */
+    int32_t shard_index;
+    int32_t packed;             /* 1: write owned tiles packed (tile-major) instead of row-major */
+} mcpt_render_params;
+
+typedef struct {
+    uint64_t rays;              /* closest-hit queries */
+    uint64_t paths;
+    uint64_t inner_visits;      /* inner KD nodes visited */
+    uint64_t leaf_visits;
+    uint64_t leaf_refs;         /* leaf triangle index reads */
+    uint64_t tri_tests;
+    uint64_t shades;            /* non-terminal hits shaded */
+    uint64_t stack_spills;      /* traversal stack entries spilled to global memory */
+    uint64_t renders;           /* render calls covered by this record */
+    double kernel_ms;           /* summed GPU time of the path kernel */
+    double reduce_ms;           /* summed GPU time of the partial-sum reduction */
+    int32_t variant;            /* kernel variant of the last call (1,2: scene in LDS; 3: global) */
+    int32_t pad_;
+} mcpt_render_stats;
+
+/* ---- library ------------------------------------------------------------ */
+int mcpt_abi_version(void);
+const char* mcpt_last_error(void);
+/* Initialize: select the HIP device(s) used by later scene_create calls on this
+ * thread (first entry becomes current).  n_devices == 0 keeps the current one. */
+int mcpt_init(const int32_t* devices, int32_t n_devices);
+int mcpt_device_count(int32_t* out);
+/* fill defaults = the CVMCTracer constants for scene 1 (CUTracer.cu:347-360) */
+void mcpt_render_params_default(mcpt_render_params* p);
+
+/* ---- host model (ObjModel) ---------------------------------------------- */
+int mcpt_model_read_obj(const char* path, mcpt_model** out);
+void mcpt_model_free(mcpt_model* m);
+int mcpt_model_get_info(const mcpt_model* m, mcpt_model_info* out);
+int mcpt_model_copy_vertices(const mcpt_model* m, float* out);       /* n_vertices*3 */
+int mcpt_model_copy_normals(const mcpt_model* m, float* out);        /* n_normals*3 */
+int mcpt_model_copy_triangles(const mcpt_model* m, int32_t* out);    /* n_triangles*10: v[3] t[3] n[3] mat */
+int mcpt_model_copy_materials(const mcpt_model* m, double* out);     /* n_materials*12: Ka Kd Ks Ns Tr Ni */
+/* group g (std::map order): name into buf, triangle count in *n; copy indices if tris != NULL */
+int mcpt_model_group(const mcpt_model* m, int64_t g, char* name_buf, int64_t name_cap,
+                     int64_t* n, int32_t* tris);
+
+/* ---- scene (CreateGeometry / DestroyGeometry) ---------------------------- */
+/* Builds geometries, the KD tree and the device image on the current device.
+ * The model is borrowed for the duration of the call only.                 */
+int mcpt_scene_create(const mcpt_model* m, mcpt_scene** out);
+/* Same, but host-only: no device allocation (KD inspection / CPU tests).   */
+int mcpt_scene_create_host(const mcpt_model* m, mcpt_scene** out);
+void mcpt_scene_destroy(mcpt_scene* s);
+int mcpt_scene_get_info(const mcpt_scene* s, mcpt_scene_info* out);
+/* KD tree as built (BFS order, QuinEngine/RTX/ShaderResource.hpp:128-179):
+ * nodes n_nodes*12 words {left,right,axis(0 leaf,1..3),split bits,min[3],max[3],
+ * leaf_begin,leaf_count}; leaf ids = kd triangle ids; kd_tris = kd id -> OBJ
+ * triangle index; geoms n_geometries*14 floats {Ka Kd Ks Ns Tr Ni start count} */
+int mcpt_scene_copy_kd(const mcpt_scene* s, uint32_t* nodes, uint32_t* leaf_ids,
+                       int32_t* kd_tris, float* geoms);
+
+/* ---- render (RenderScene) ------------------------------------------------- */
+/* Synchronous; fb_rgb is caller-owned host memory, width*height*3 floats
+ * (or, when packed/sharded, owned-pixel-count*3).  Reads fb_rgb when
+ * prev_count > 0.  stats may be NULL.                                        */
+int mcpt_render(mcpt_scene* s, const mcpt_render_params* p, float* fb_rgb, mcpt_render_stats* stats);
+/* Asynchronous on hip_stream (a hipStream_t, NULL = default stream);
+ * d_fb_rgba is device memory, 4 floats per output pixel.  Counters and
+ * kernel times accumulate until mcpt_render_stats_read(), which waits for
+ * the outstanding calls and resets them.                                   */
+int mcpt_render_device(mcpt_scene* s, const mcpt_render_params* p, float* d_fb_rgba, void* hip_stream);
+int mcpt_render_stats_read(mcpt_scene* s, mcpt_render_stats* out);
+/* Diagnostics: synchronous render that also returns, per work unit
+ * u = chunk*pixels + pixel, {rays, inner visits, leaf visits, tri tests}
+ * (unit_counters: total_units*4 uint32, total_units = pixels * ceil(spp/chunk)). */
+int mcpt_render_unit_counters(mcpt_scene* s, const mcpt_render_params* p, float* fb_rgb,
+                              uint32_t* unit_counters);
+/* number of output pixels a (sharded) render writes, and their (x,y) list */
+int64_t mcpt_shard_pixel_count(const mcpt_render_params* p);
+int mcpt_shard_pixels(const mcpt_render_params* p, int32_t* xy);      /* count*2 */
+/* reserve device workspace for p so mcpt_render_device allocates nothing
+ * (required before hipGraph capture)                                       */
+int mcpt_scene_reserve(mcpt_scene* s, const mcpt_render_params* p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MCPT_H */

@@ -1,0 +1,72 @@
+"""Build libmcpt.so (HIP for gfx950 + C++ host) in-tree with hipcc.
+
+Output: montecarlopathtracer_amd/lib/libmcpt.so.  Every translation unit is
+compiled with -ffp-contract=off and without fast-math: the kernel's float
+arithmetic must round exactly as the specification.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+LIBDIR = os.path.join(HERE, "lib")
+LIB = os.path.join(LIBDIR, "libmcpt.so")
+SOURCES = ["host_model.cpp", "capi.cpp", "render.hip"]
+HEADERS = ["host_model.hpp", "mcpt_device.hpp", "render_launch.hpp"]
+ARCH = os.environ.get("MCPT_OFFLOAD_ARCH", "gfx950")
+
+COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-Wall",
+          "-I" + os.path.join(ROOT, "include")]
+
+
+def _hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
+        if c and (os.path.sep not in c or os.path.exists(c)):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def _stale() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(ROOT, "include", "mcpt.h")]
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not _stale():
+        return LIB
+    os.makedirs(os.path.join(LIBDIR, "obj"), exist_ok=True)
+    hipcc = _hipcc()
+
+    def compile_one(src):
+        obj = os.path.join(LIBDIR, "obj", src + ".o")
+        lang = (["-x", "hip", f"--offload-arch={ARCH}"] if src.endswith(".hip")
+                else ["-x", "c++", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include"])
+        cmd = [hipcc] + lang + COMMON + ["-c", os.path.join(CSRC, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"compile failed: {src}\n{r.stdout}\n{r.stderr}")
+        return obj
+
+    with ThreadPoolExecutor(max_workers=len(SOURCES)) as ex:
+        objs = list(ex.map(compile_one, SOURCES))
+    tmp = LIB + f".{os.getpid()}.tmp"
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed\n{r.stdout}\n{r.stderr}")
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,606 @@
+// capi.cpp -- implementation of the C ABI declared in include/mcpt.h.
+//
+// Host side of the reference's PW::Tracer module (CVMCTracer/CUDA/CUTracer.cu:
+// 220-404): device selection, scene upload (CreateGeometry), teardown
+// (DestroyGeometry, here freeing exactly what was allocated) and the render
+// entry (RenderScene).  Unlike the reference, no module globals hold the scene:
+// every call takes the opaque handle it works on.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/mcpt.h"
+#include "host_model.hpp"
+#include "render_launch.hpp"
+
+struct mcpt_model {
+    mcpt::ObjModel m;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                   \
+    do {                                                                                \
+        hipError_t e_ = (expr);                                                         \
+        if (e_ != hipSuccess)                                                           \
+            throw mcpt::Error{MCPT_E_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)}; \
+    } while (0)
+
+template <typename F>
+int guarded(F&& f) {
+    try {
+        return f();
+    } catch (const mcpt::Error& e) {
+        return fail(e.code, e.msg);
+    } catch (const std::bad_alloc&) {
+        return fail(MCPT_E_NOMEM, "out of host memory");
+    } catch (const std::exception& e) {
+        return fail(MCPT_E_INVALID, e.what());
+    }
+}
+
+uint32_t tea16(uint32_t v0, uint32_t v1) {   // MCRT/QuinEngine/Shader/rtx.hlsl:61-72
+    uint32_t sum = 0;
+    for (int n = 0; n < 16; n++) {
+        sum += 0x9e3779b9u;
+        v0 += ((v1 << 4) + 0xa341316cu) ^ (v1 + sum) ^ ((v1 >> 5) + 0xc8013ea4u);
+        v1 += ((v0 << 4) + 0xad90777du) ^ (v0 + sum) ^ ((v0 >> 5) + 0x7e95761eu);
+    }
+    return v0;
+}
+
+struct Vf {
+    float x, y, z;
+};
+// Math::Vector3f::normal()/cross() (CVMCTracer/Framework/Math.hpp:112-123)
+Vf normal_of(Vf v) {
+    float len = std::sqrt(v.x * v.x + v.y * v.y + v.z * v.z);
+    float d = std::fmax(len, FLT_MIN);
+    return Vf{v.x / d, v.y / d, v.z / d};
+}
+Vf cross_of(Vf a, Vf b) { return Vf{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+
+struct Workspace {
+    void* partial = nullptr;
+    size_t partial_bytes = 0;
+    void* small = nullptr;       // counter (16 B) + stats (64 B)
+    void* spill = nullptr;
+    size_t spill_bytes = 0;
+    void* fb = nullptr;          // mcpt_render staging framebuffer
+    size_t fb_bytes = 0;
+};
+
+struct Timing {
+    hipEvent_t e[3];
+};
+
+}  // namespace
+
+struct mcpt_scene {
+    mcpt::HostScene hs;
+    bool on_device = false;
+    int device = -1;
+    int cus = 0;
+    std::vector<unsigned char> image;   // host copy of the device image
+    mcpt::GpuScene gpu{};
+    void* d_image = nullptr;
+    void* d_normals = nullptr;
+    Workspace ws;
+    std::vector<Timing> pending, free_timing;
+    int last_variant = 0;
+    uint64_t renders = 0;
+
+    ~mcpt_scene() {
+        if (!on_device) return;
+        int prev = -1;
+        (void)hipGetDevice(&prev);
+        (void)hipSetDevice(device);
+        (void)hipDeviceSynchronize();
+        for (void* p : {d_image, d_normals, ws.partial, ws.small, ws.spill, ws.fb})
+            if (p) (void)hipFree(p);
+        for (auto& t : pending) for (auto ev : t.e) (void)hipEventDestroy(ev);
+        for (auto& t : free_timing) for (auto ev : t.e) (void)hipEventDestroy(ev);
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+namespace {
+
+void build_image(mcpt_scene& s) {
+    const mcpt::HostScene& hs = s.hs;
+    const uint32_t nt = static_cast<uint32_t>(hs.kd_tris.size());
+    const uint32_t nn = static_cast<uint32_t>(hs.nodes.size());
+    const uint32_t nl = static_cast<uint32_t>(hs.leaf_ids.size());
+    const uint32_t ng = static_cast<uint32_t>(hs.geoms.size());
+    auto al16 = [](size_t x) { return (x + 15u) & ~size_t(15); };
+    const size_t off_tris = 0;
+    const size_t off_nodes = al16(off_tris + size_t(nt) * 48);
+    const size_t off_leafs = al16(off_nodes + size_t(nn) * 8);
+    const size_t off_geoms = al16(off_leafs + size_t(nl) * 4);
+    const size_t total = al16(off_geoms + size_t(ng) * 64);
+    if (total > 0xFFFFFFF0u) throw mcpt::Error{MCPT_E_UNSUPPORTED, "scene image exceeds 4 GiB"};
+    if (nn >= (1u << 30) || nl >= (1u << 30)) throw mcpt::Error{MCPT_E_UNSUPPORTED, "KD tree too large"};
+    s.image.assign(total, 0);
+    unsigned char* img = s.image.data();
+    for (uint32_t k = 0; k < nt; ++k) {
+        const float* v = &hs.kd_verts[9 * size_t(k)];
+        float rec[12] = {v[0], v[1], v[2], 0.0f,
+                         v[0] - v[3], v[1] - v[4], v[2] - v[5], 0.0f,
+                         v[0] - v[6], v[1] - v[7], v[2] - v[8], 0.0f};
+        std::memcpy(&rec[3], &hs.kd_prio[k], 4);
+        std::memcpy(&rec[7], &hs.kd_geom[k], 4);
+        std::memcpy(img + off_tris + size_t(k) * 48, rec, 48);
+    }
+    for (uint32_t i = 0; i < nn; ++i) {
+        const mcpt::KdNode& n = hs.nodes[i];
+        uint32_t w[2];
+        if (n.axis) {
+            w[0] = ((n.axis - 1u) << 30) | n.left;
+            std::memcpy(&w[1], &n.split, 4);
+        } else {
+            w[0] = (3u << 30) | n.leaf_begin;
+            w[1] = n.leaf_count;
+        }
+        std::memcpy(img + off_nodes + size_t(i) * 8, w, 8);
+    }
+    if (nl) std::memcpy(img + off_leafs, hs.leaf_ids.data(), size_t(nl) * 4);
+    for (uint32_t g = 0; g < ng; ++g) {
+        const mcpt::Geometry& ge = hs.geoms[g];
+        mcpt::GpuGeom gg{};
+        gg.Ka[0] = ge.Ka.x; gg.Ka[1] = ge.Ka.y; gg.Ka[2] = ge.Ka.z;
+        gg.Kd[0] = ge.Kd.x; gg.Kd[1] = ge.Kd.y; gg.Kd[2] = ge.Kd.z;
+        gg.Ks[0] = ge.Ks.x; gg.Ks[1] = ge.Ks.y; gg.Ks[2] = ge.Ks.z;
+        gg.Ns = ge.Ns; gg.Tr = ge.Tr; gg.Ni = ge.Ni;
+        gg.Ns_u = ge.Ns > 0.0f ? (ge.Ns < 4294967040.0f ? static_cast<uint32_t>(ge.Ns) : 0xFFFFFF00u) : 0u;
+        std::memcpy(img + off_geoms + size_t(g) * 64, &gg, 64);
+    }
+    mcpt::GpuScene& gs = s.gpu;
+    gs.image_bytes = static_cast<uint32_t>(total);
+    gs.off_tris = static_cast<uint32_t>(off_tris);
+    gs.off_nodes = static_cast<uint32_t>(off_nodes);
+    gs.off_leafs = static_cast<uint32_t>(off_leafs);
+    gs.off_geoms = static_cast<uint32_t>(off_geoms);
+    gs.n_tris = nt; gs.n_nodes = nn; gs.n_leafs = nl; gs.n_geoms = ng;
+    if (nn) {
+        for (int a = 0; a < 3; ++a) { gs.root_min[a] = hs.nodes[0].bmin[a]; gs.root_max[a] = hs.nodes[0].bmax[a]; }
+    }
+}
+
+void ensure_buf(void*& p, size_t& have, size_t need) {
+    if (have >= need && p) return;
+    if (p) HIP_TRY(hipFree(p));
+    p = nullptr;
+    have = 0;
+    HIP_TRY(hipMalloc(&p, need ? need : 16));
+    have = need;
+}
+
+struct Plan {
+    mcpt::KernelParams kp;
+    size_t out_pixels;
+};
+
+Plan make_plan(const mcpt_scene& s, const mcpt_render_params* p) {
+    if (!p) throw mcpt::Error{MCPT_E_INVALID, "params is NULL"};
+    if (p->width <= 0 || p->height <= 0) throw mcpt::Error{MCPT_E_INVALID, "width/height must be positive"};
+    if (p->spp == 0) throw mcpt::Error{MCPT_E_INVALID, "spp must be > 0"};
+    if (p->max_depth < 0 || p->max_depth > 1000) throw mcpt::Error{MCPT_E_INVALID, "max_depth out of range"};
+    const int T = p->tile > 0 ? p->tile : 8;
+    if (T > 256) throw mcpt::Error{MCPT_E_INVALID, "tile too large"};
+    const int sc = p->shard_count > 1 ? p->shard_count : 1;
+    const int si = sc > 1 ? p->shard_index : 0;
+    if (si < 0 || si >= sc) throw mcpt::Error{MCPT_E_INVALID, "shard_index out of range"};
+    const uint64_t tiles_x = (uint64_t(p->width) + T - 1) / T, tiles_y = (uint64_t(p->height) + T - 1) / T;
+    const uint64_t ntiles = tiles_x * tiles_y;
+    const uint64_t owned = uint64_t(si) < ntiles ? (ntiles - uint64_t(si) + uint64_t(sc) - 1) / uint64_t(sc) : 0;
+    const uint64_t npix = owned * uint64_t(T) * uint64_t(T);
+    const uint32_t chunk = p->spp_chunk ? (p->spp_chunk < p->spp ? p->spp_chunk : p->spp) : p->spp;
+    const uint64_t nchunks = (uint64_t(p->spp) + chunk - 1) / chunk;
+    if (npix * nchunks >= 0xFFFFFFFFull) throw mcpt::Error{MCPT_E_UNSUPPORTED, "too many work units for one call"};
+
+    Plan pl;
+    mcpt::KernelParams& k = pl.kp;
+    std::memset(&k, 0, sizeof k);
+    k.scene = s.gpu;
+    k.width = p->width; k.height = p->height;
+    k.tile = T; k.tiles_x = static_cast<int32_t>(tiles_x);
+    k.shard_count = sc; k.shard_index = si;
+    k.packed = (p->packed || sc > 1) ? 1 : 0;
+    k.npix_local = static_cast<uint32_t>(npix);
+    k.spp = p->spp; k.spp_offset = p->spp_offset; k.chunk = chunk;
+    k.nchunks = static_cast<uint32_t>(nchunks);
+    k.total_units = static_cast<uint32_t>(npix * nchunks);
+    k.max_depth = p->max_depth;
+    k.illum = p->illum;
+    const float a = p->fov_deg * 3.14159265359f / 360;   // CUTracer.cu:189,202
+    k.tan_half_fov = static_cast<float>(std::tan(static_cast<double>(a)));
+    k.fresnel_kd = p->fresnel_kd ? 1 : 0;
+    k.prev_count = p->prev_count;
+    // camera basis (CUTracer.cu:349-359)
+    Vf d = normal_of(Vf{p->dir[0], p->dir[1], p->dir[2]});
+    Vf r = normal_of(cross_of(d, Vf{p->up[0], p->up[1], p->up[2]}));
+    Vf u = normal_of(cross_of(r, d));
+    for (int i = 0; i < 3; ++i) k.eye[i] = p->eye[i];
+    k.fwd[0] = d.x; k.fwd[1] = d.y; k.fwd[2] = d.z;
+    k.up[0] = u.x; k.up[1] = u.y; k.up[2] = u.z;
+    k.right[0] = r.x; k.right[1] = r.y; k.right[2] = r.z;
+    k.key = tea16(static_cast<uint32_t>(p->seed), static_cast<uint32_t>(p->seed >> 32));
+    pl.out_pixels = k.packed ? size_t(npix) : size_t(p->width) * size_t(p->height);
+    return pl;
+}
+
+void prepare_workspace(mcpt_scene& s, mcpt::KernelParams& k) {
+    ensure_buf(s.ws.partial, s.ws.partial_bytes, size_t(k.nchunks) * k.npix_local * 16);
+    if (!s.ws.small) {
+        HIP_TRY(hipMalloc(&s.ws.small, 128));
+        HIP_TRY(hipMemset(s.ws.small, 0, 128));
+    }
+    const size_t lanes = static_cast<size_t>(mcpt::total_lanes_for(s.gpu.image_bytes, s.cus));
+    ensure_buf(s.ws.spill, s.ws.spill_bytes, 32 * lanes * 16);
+    k.partial = static_cast<float4*>(s.ws.partial);
+    k.counter = static_cast<uint32_t*>(s.ws.small);
+    k.stats = reinterpret_cast<unsigned long long*>(static_cast<char*>(s.ws.small) + 64);
+    k.spill = static_cast<uint4*>(s.ws.spill);
+}
+
+void set_device(const mcpt_scene& s) {
+    int cur = -1;
+    HIP_TRY(hipGetDevice(&cur));
+    if (cur != s.device) HIP_TRY(hipSetDevice(s.device));
+}
+
+void render_async(mcpt_scene& s, const mcpt_render_params* p, float* d_fb, hipStream_t st,
+                  uint32_t* d_unit_counters = nullptr) {
+    if (!s.on_device) throw mcpt::Error{MCPT_E_INVALID, "scene was created host-only"};
+    if (!d_fb) throw mcpt::Error{MCPT_E_INVALID, "framebuffer is NULL"};
+    set_device(s);
+    Plan pl = make_plan(s, p);
+    prepare_workspace(s, pl.kp);
+    pl.kp.unit_counters = d_unit_counters;
+    Timing t;
+    if (!s.free_timing.empty()) {
+        t = s.free_timing.back();
+        s.free_timing.pop_back();
+    } else {
+        for (auto& ev : t.e) HIP_TRY(hipEventCreate(&ev));
+    }
+    HIP_TRY(mcpt::launch_render(pl.kp, s.cus, st, t.e[0], t.e[1], t.e[2], reinterpret_cast<float4*>(d_fb),
+                                &s.last_variant));
+    s.pending.push_back(t);
+    s.renders++;
+}
+
+void read_stats(mcpt_scene& s, mcpt_render_stats* out) {
+    set_device(s);
+    mcpt_render_stats r;
+    std::memset(&r, 0, sizeof r);
+    double kms = 0, rms = 0;
+    for (auto& t : s.pending) {
+        HIP_TRY(hipEventSynchronize(t.e[2]));
+        float a = 0, b = 0;
+        HIP_TRY(hipEventElapsedTime(&a, t.e[0], t.e[1]));
+        HIP_TRY(hipEventElapsedTime(&b, t.e[1], t.e[2]));
+        kms += a;
+        rms += b;
+        s.free_timing.push_back(t);
+    }
+    s.pending.clear();
+    if (s.ws.small) {
+        unsigned long long st[8];
+        HIP_TRY(hipMemcpy(st, static_cast<char*>(s.ws.small) + 64, sizeof st, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemset(static_cast<char*>(s.ws.small) + 64, 0, 64));
+        r.rays = st[0]; r.paths = st[1]; r.inner_visits = st[2]; r.leaf_visits = st[3];
+        r.leaf_refs = st[4]; r.tri_tests = st[5]; r.shades = st[6]; r.stack_spills = st[7];
+    }
+    r.renders = s.renders;
+    s.renders = 0;
+    r.kernel_ms = kms;
+    r.reduce_ms = rms;
+    r.variant = s.last_variant;
+    if (out) *out = r;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mcpt_abi_version(void) { return MCPT_ABI_VERSION; }
+
+const char* mcpt_last_error(void) { return g_err.c_str(); }
+
+int mcpt_init(const int32_t* devices, int32_t n) {
+    return guarded([&]() -> int {
+        if (n < 0 || (n > 0 && !devices)) return fail(MCPT_E_INVALID, "bad device list");
+        if (n == 0) return MCPT_OK;
+        int count = 0;
+        HIP_TRY(hipGetDeviceCount(&count));
+        for (int i = 0; i < n; ++i)
+            if (devices[i] < 0 || devices[i] >= count) return fail(MCPT_E_INVALID, "device ordinal out of range");
+        HIP_TRY(hipSetDevice(devices[0]));
+        return MCPT_OK;
+    });
+}
+
+int mcpt_device_count(int32_t* out) {
+    return guarded([&]() -> int {
+        if (!out) return fail(MCPT_E_INVALID, "out is NULL");
+        int c = 0;
+        HIP_TRY(hipGetDeviceCount(&c));
+        *out = c;
+        return MCPT_OK;
+    });
+}
+
+void mcpt_render_params_default(mcpt_render_params* p) {
+    if (!p) return;
+    std::memset(p, 0, sizeof *p);
+    p->width = 800; p->height = 600;                 // CV/stdafx.h:41-42
+    p->spp = 100;                                     // NUM_SAMPLES_PER_KERNEL
+    p->max_depth = 7;                                 // CUTracer.cu:212
+    p->illum = 10.0f;                                 // ILLUM
+    p->fov_deg = 60.0f;                               // CUTracer.cu:189
+    p->eye[0] = 0; p->eye[1] = 5; p->eye[2] = 17;     // scene 1 camera, CUTracer.cu:349-351
+    p->dir[0] = 0; p->dir[1] = 0; p->dir[2] = -1;
+    p->up[0] = 0; p->up[1] = 1; p->up[2] = 0;
+    p->seed = 0x4D435054ull;
+    p->fresnel_kd = 1;
+    p->tile = 8;
+    p->shard_count = 1;
+}
+
+int mcpt_model_read_obj(const char* path, mcpt_model** out) {
+    return guarded([&]() -> int {
+        if (!path || !out) return fail(MCPT_E_INVALID, "path/out is NULL");
+        auto m = std::make_unique<mcpt_model>();
+        mcpt::read_obj(path, m->m);
+        *out = m.release();
+        return MCPT_OK;
+    });
+}
+
+void mcpt_model_free(mcpt_model* m) { delete m; }
+
+int mcpt_model_get_info(const mcpt_model* m, mcpt_model_info* out) {
+    if (!m || !out) return fail(MCPT_E_INVALID, "NULL argument");
+    out->n_vertices = static_cast<int64_t>(m->m.vertices.size());
+    out->n_normals = static_cast<int64_t>(m->m.normals.size());
+    out->n_texcoords = m->m.n_texcoords;
+    out->n_triangles = static_cast<int64_t>(m->m.triangles.size());
+    out->n_materials = static_cast<int64_t>(m->m.materials.size());
+    out->n_groups = static_cast<int64_t>(m->m.groups.size());
+    return MCPT_OK;
+}
+
+int mcpt_model_copy_vertices(const mcpt_model* m, float* out) {
+    if (!m || !out) return fail(MCPT_E_INVALID, "NULL argument");
+    for (size_t i = 0; i < m->m.vertices.size(); ++i) {
+        out[3 * i] = m->m.vertices[i].x; out[3 * i + 1] = m->m.vertices[i].y; out[3 * i + 2] = m->m.vertices[i].z;
+    }
+    return MCPT_OK;
+}
+
+int mcpt_model_copy_normals(const mcpt_model* m, float* out) {
+    if (!m || !out) return fail(MCPT_E_INVALID, "NULL argument");
+    for (size_t i = 0; i < m->m.normals.size(); ++i) {
+        out[3 * i] = m->m.normals[i].x; out[3 * i + 1] = m->m.normals[i].y; out[3 * i + 2] = m->m.normals[i].z;
+    }
+    return MCPT_OK;
+}
+
+int mcpt_model_copy_triangles(const mcpt_model* m, int32_t* out) {
+    if (!m || !out) return fail(MCPT_E_INVALID, "NULL argument");
+    for (size_t i = 0; i < m->m.triangles.size(); ++i) {
+        const auto& t = m->m.triangles[i];
+        for (int j = 0; j < 3; ++j) { out[10 * i + j] = t.v[j]; out[10 * i + 3 + j] = t.t[j]; out[10 * i + 6 + j] = t.n[j]; }
+        out[10 * i + 9] = t.material;
+    }
+    return MCPT_OK;
+}
+
+int mcpt_model_copy_materials(const mcpt_model* m, double* out) {
+    if (!m || !out) return fail(MCPT_E_INVALID, "NULL argument");
+    for (size_t i = 0; i < m->m.materials.size(); ++i) {
+        const auto& t = m->m.materials[i];
+        double* o = out + 12 * i;
+        o[0] = t.Ka.x; o[1] = t.Ka.y; o[2] = t.Ka.z; o[3] = t.Kd.x; o[4] = t.Kd.y; o[5] = t.Kd.z;
+        o[6] = t.Ks.x; o[7] = t.Ks.y; o[8] = t.Ks.z; o[9] = t.Ns; o[10] = t.Tr; o[11] = t.Ni;
+    }
+    return MCPT_OK;
+}
+
+int mcpt_model_group(const mcpt_model* m, int64_t g, char* name_buf, int64_t name_cap, int64_t* n, int32_t* tris) {
+    if (!m || g < 0 || g >= static_cast<int64_t>(m->m.groups.size())) return fail(MCPT_E_INVALID, "bad group index");
+    auto it = m->m.groups.begin();
+    std::advance(it, g);
+    if (name_buf && name_cap > 0) std::snprintf(name_buf, static_cast<size_t>(name_cap), "%s", it->first.c_str());
+    if (n) *n = static_cast<int64_t>(it->second.size());
+    if (tris) std::memcpy(tris, it->second.data(), it->second.size() * sizeof(int32_t));
+    return MCPT_OK;
+}
+
+static int scene_create_impl(const mcpt_model* m, mcpt_scene** out, bool device) {
+    return guarded([&]() -> int {
+        if (!m || !out) return fail(MCPT_E_INVALID, "NULL argument");
+        auto s = std::make_unique<mcpt_scene>();
+        mcpt::build_host_scene(m->m, s->hs);
+        if (s->hs.kd_tris.empty()) return fail(MCPT_E_INVALID, "scene has no triangles");
+        build_image(*s);
+        if (device) {
+            HIP_TRY(hipGetDevice(&s->device));
+            HIP_TRY(hipDeviceGetAttribute(&s->cus, hipDeviceAttributeMultiprocessorCount, s->device));
+            s->on_device = true;
+            HIP_TRY(hipMalloc(&s->d_image, s->image.size()));
+            HIP_TRY(hipMemcpy(s->d_image, s->image.data(), s->image.size(), hipMemcpyHostToDevice));
+            const size_t nt = s->hs.kd_tris.size();
+            std::vector<float> nrm(nt * 12, 0.0f);
+            for (size_t k = 0; k < nt; ++k)
+                for (int j = 0; j < 3; ++j)
+                    for (int c = 0; c < 3; ++c) nrm[12 * k + 4 * j + c] = s->hs.kd_normals[9 * k + 3 * j + c];
+            HIP_TRY(hipMalloc(&s->d_normals, nrm.size() * 4));
+            HIP_TRY(hipMemcpy(s->d_normals, nrm.data(), nrm.size() * 4, hipMemcpyHostToDevice));
+            s->gpu.image = static_cast<const unsigned char*>(s->d_image);
+            s->gpu.normals = static_cast<const float4*>(s->d_normals);
+        }
+        *out = s.release();
+        return MCPT_OK;
+    });
+}
+
+int mcpt_scene_create(const mcpt_model* m, mcpt_scene** out) { return scene_create_impl(m, out, true); }
+int mcpt_scene_create_host(const mcpt_model* m, mcpt_scene** out) { return scene_create_impl(m, out, false); }
+
+void mcpt_scene_destroy(mcpt_scene* s) { delete s; }
+
+int mcpt_scene_get_info(const mcpt_scene* s, mcpt_scene_info* out) {
+    if (!s || !out) return fail(MCPT_E_INVALID, "NULL argument");
+    out->n_geometries = static_cast<int64_t>(s->hs.geoms.size());
+    out->n_triangles = static_cast<int64_t>(s->hs.kd_tris.size());
+    out->n_nodes = static_cast<int64_t>(s->hs.nodes.size());
+    out->n_leaf_refs = static_cast<int64_t>(s->hs.leaf_ids.size());
+    out->kd_depth = s->hs.kd_depth;
+    out->lds_bytes = mcpt::lds_bytes_in_lds(s->gpu.image_bytes, 4) <= mcpt::kMaxLds ? s->gpu.image_bytes : 0;
+    out->device = s->device;
+    return MCPT_OK;
+}
+
+int mcpt_scene_copy_kd(const mcpt_scene* s, uint32_t* nodes, uint32_t* leaf_ids, int32_t* kd_tris, float* geoms) {
+    if (!s) return fail(MCPT_E_INVALID, "NULL scene");
+    const auto& hs = s->hs;
+    if (nodes)
+        for (size_t i = 0; i < hs.nodes.size(); ++i) {
+            const auto& n = hs.nodes[i];
+            uint32_t* o = nodes + 12 * i;
+            o[0] = n.left; o[1] = n.right; o[2] = n.axis;
+            std::memcpy(&o[3], &n.split, 4);
+            std::memcpy(&o[4], n.bmin, 12);
+            std::memcpy(&o[7], n.bmax, 12);
+            o[10] = n.leaf_begin; o[11] = n.leaf_count;
+        }
+    if (leaf_ids && !hs.leaf_ids.empty()) std::memcpy(leaf_ids, hs.leaf_ids.data(), hs.leaf_ids.size() * 4);
+    if (kd_tris) std::memcpy(kd_tris, hs.kd_tris.data(), hs.kd_tris.size() * 4);
+    if (geoms)
+        for (size_t g = 0; g < hs.geoms.size(); ++g) {
+            const auto& e = hs.geoms[g];
+            float* o = geoms + 14 * g;
+            o[0] = e.Ka.x; o[1] = e.Ka.y; o[2] = e.Ka.z; o[3] = e.Kd.x; o[4] = e.Kd.y; o[5] = e.Kd.z;
+            o[6] = e.Ks.x; o[7] = e.Ks.y; o[8] = e.Ks.z; o[9] = e.Ns; o[10] = e.Tr; o[11] = e.Ni;
+            o[12] = static_cast<float>(e.start); o[13] = static_cast<float>(e.count);
+        }
+    return MCPT_OK;
+}
+
+int mcpt_render_device(mcpt_scene* s, const mcpt_render_params* p, float* d_fb_rgba, void* hip_stream) {
+    return guarded([&]() -> int {
+        if (!s) return fail(MCPT_E_INVALID, "NULL scene");
+        render_async(*s, p, d_fb_rgba, static_cast<hipStream_t>(hip_stream));
+        return MCPT_OK;
+    });
+}
+
+int mcpt_render_stats_read(mcpt_scene* s, mcpt_render_stats* out) {
+    return guarded([&]() -> int {
+        if (!s || !s->on_device) return fail(MCPT_E_INVALID, "scene is not on a device");
+        read_stats(*s, out);
+        return MCPT_OK;
+    });
+}
+
+static int render_sync(mcpt_scene* s, const mcpt_render_params* p, float* fb_rgb, mcpt_render_stats* stats,
+                       uint32_t* unit_counters) {
+    return guarded([&]() -> int {
+        if (!s || !fb_rgb) return fail(MCPT_E_INVALID, "NULL argument");
+        if (!s->on_device) return fail(MCPT_E_INVALID, "scene was created host-only");
+        set_device(*s);
+        Plan pl = make_plan(*s, p);
+        const size_t npx = pl.out_pixels;
+        ensure_buf(s->ws.fb, s->ws.fb_bytes, npx * 16);
+        std::vector<float> rgba(npx * 4, 0.0f);
+        if (p->prev_count > 0) {
+            for (size_t i = 0; i < npx; ++i)
+                for (int c = 0; c < 3; ++c) rgba[4 * i + c] = fb_rgb[3 * i + c];
+            HIP_TRY(hipMemcpy(s->ws.fb, rgba.data(), npx * 16, hipMemcpyHostToDevice));
+        } else {
+            HIP_TRY(hipMemset(s->ws.fb, 0, npx * 16));
+        }
+        read_stats(*s, nullptr);   // start a fresh record
+        void* d_uc = nullptr;
+        const size_t uc_bytes = size_t(pl.kp.total_units) * 16;
+        if (unit_counters) {
+            HIP_TRY(hipMalloc(&d_uc, uc_bytes ? uc_bytes : 16));
+            HIP_TRY(hipMemset(d_uc, 0, uc_bytes ? uc_bytes : 16));
+        }
+        render_async(*s, p, static_cast<float*>(s->ws.fb), nullptr, static_cast<uint32_t*>(d_uc));
+        HIP_TRY(hipStreamSynchronize(nullptr));
+        if (unit_counters) {
+            HIP_TRY(hipMemcpy(unit_counters, d_uc, uc_bytes, hipMemcpyDeviceToHost));
+            HIP_TRY(hipFree(d_uc));
+        }
+        HIP_TRY(hipMemcpy(rgba.data(), s->ws.fb, npx * 16, hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < npx; ++i)
+            for (int c = 0; c < 3; ++c) fb_rgb[3 * i + c] = rgba[4 * i + c];
+        read_stats(*s, stats);
+        return MCPT_OK;
+    });
+}
+
+int mcpt_render(mcpt_scene* s, const mcpt_render_params* p, float* fb_rgb, mcpt_render_stats* stats) {
+    return render_sync(s, p, fb_rgb, stats, nullptr);
+}
+
+int mcpt_render_unit_counters(mcpt_scene* s, const mcpt_render_params* p, float* fb_rgb, uint32_t* unit_counters) {
+    if (!unit_counters) return fail(MCPT_E_INVALID, "unit_counters is NULL");
+    return render_sync(s, p, fb_rgb, nullptr, unit_counters);
+}
+
+int64_t mcpt_shard_pixel_count(const mcpt_render_params* p) {
+    if (!p || p->width <= 0 || p->height <= 0) return fail(MCPT_E_INVALID, "bad params");
+    const int64_t T = p->tile > 0 ? p->tile : 8;
+    const int64_t sc = p->shard_count > 1 ? p->shard_count : 1, si = sc > 1 ? p->shard_index : 0;
+    if (si < 0 || si >= sc) return fail(MCPT_E_INVALID, "shard_index out of range");
+    const int64_t ntiles = ((p->width + T - 1) / T) * ((p->height + T - 1) / T);
+    const int64_t owned = si < ntiles ? (ntiles - si + sc - 1) / sc : 0;
+    return owned * T * T;
+}
+
+int mcpt_shard_pixels(const mcpt_render_params* p, int32_t* xy) {
+    const int64_t n = mcpt_shard_pixel_count(p);
+    if (n < 0) return static_cast<int>(n);
+    if (!xy) return fail(MCPT_E_INVALID, "xy is NULL");
+    const int64_t T = p->tile > 0 ? p->tile : 8;
+    const int64_t sc = p->shard_count > 1 ? p->shard_count : 1, si = sc > 1 ? p->shard_index : 0;
+    const int64_t tiles_x = (p->width + T - 1) / T;
+    for (int64_t v = 0; v < n; ++v) {
+        const int64_t k = v / (T * T), w = v % (T * T);
+        const int64_t t = si + k * sc;
+        const int64_t x = (t % tiles_x) * T + w % T, y = (t / tiles_x) * T + w / T;
+        const bool in = x < p->width && y < p->height;
+        xy[2 * v] = in ? static_cast<int32_t>(x) : -1;
+        xy[2 * v + 1] = in ? static_cast<int32_t>(y) : -1;
+    }
+    return MCPT_OK;
+}
+
+int mcpt_scene_reserve(mcpt_scene* s, const mcpt_render_params* p) {
+    return guarded([&]() -> int {
+        if (!s || !s->on_device) return fail(MCPT_E_INVALID, "scene is not on a device");
+        set_device(*s);
+        Plan pl = make_plan(*s, p);
+        prepare_workspace(*s, pl.kp);
+        return MCPT_OK;
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,455 @@
+// host_model.cpp -- OBJ/MTL reader, CreateGeometry tables and the KD-tree build.
+//
+// Reader semantics: CVMCTracer/CVMCTracer/Framework/ObjReader.cpp:8-259 and
+// ObjReader.hpp:37-139 (dummy index 0, map-ordered groups, fan triangulation,
+// "Ks" implies Ns=2, newmtl re-uses an existing name).  Numbers are parsed
+// with strtof/strtod, which is what std::istream >> float/double resolves to.
+//
+// KD build semantics: MCRT/QuinEngine/Utils/KDTree.hpp:58-287 -- see
+// build_kdtree() below; the BFS flatten follows RTX/ShaderResource.hpp:128-179.
+#include "host_model.hpp"
+
+#include <algorithm>
+#include <cctype>
+#include <cfloat>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <fstream>
+#include <numeric>
+#include <sstream>
+
+#include "../../include/mcpt.h"
+
+namespace mcpt {
+namespace {
+
+// ---- whitespace tokenizer with istream-like extraction ---------------------
+struct Cursor {
+    const char* p;
+    const char* end;
+    bool fail = false;
+
+    void skip() {
+        while (p < end && std::isspace(static_cast<unsigned char>(*p))) ++p;
+    }
+    bool token(std::string& out) {          // operator>>(std::string&)
+        if (fail) return false;
+        skip();
+        if (p >= end) { fail = true; return false; }
+        const char* b = p;
+        while (p < end && !std::isspace(static_cast<unsigned char>(*p))) ++p;
+        out.assign(b, p);
+        return true;
+    }
+    // operator>>(float&) / (double&): value 0 on failure
+    template <typename T>
+    T number() {
+        if (fail) return T(0);
+        skip();
+        std::string tmp(p, std::min<size_t>(static_cast<size_t>(end - p), 128));
+        char* e = nullptr;
+        T v;
+        if constexpr (std::is_same<T, float>::value) v = std::strtof(tmp.c_str(), &e);
+        else v = std::strtod(tmp.c_str(), &e);
+        if (e == tmp.c_str()) { fail = true; return T(0); }
+        p += (e - tmp.c_str());
+        return v;
+    }
+};
+
+// ObjReader.hpp:90-138 ("v", "v/t", "v//n", "v/t/n")
+bool parse_face_vertex(const std::string& tok, int32_t& v, int32_t& t, int32_t& n) {
+    const char* s = tok.c_str();
+    auto get_int = [&](int32_t& out) -> bool {
+        const char* q = s;
+        if (*q == '+' || *q == '-') ++q;
+        if (!std::isdigit(static_cast<unsigned char>(*q))) { out = 0; return false; }
+        char* e = nullptr;
+        out = static_cast<int32_t>(std::strtol(s, &e, 10));
+        s = e;
+        return true;
+    };
+    auto get_char = [&]() -> bool {
+        while (*s && std::isspace(static_cast<unsigned char>(*s))) ++s;
+        if (!*s) return false;
+        ++s;
+        return true;
+    };
+    if (!get_int(v)) return false;
+    if (!get_char()) { t = 0; n = 0; return true; }
+    if (!get_int(t)) {
+        t = 0;
+        get_char();
+        return get_int(n);
+    }
+    if (!get_char()) { n = 0; return true; }
+    return get_int(n);
+}
+
+std::string slurp(const std::string& path) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f.is_open()) throw Error{MCPT_E_IO, "Can't open file " + path};
+    std::ostringstream ss;
+    ss << f.rdbuf();
+    return ss.str();
+}
+
+// std::getline with trailing-backslash continuation (ObjReader.cpp:23-34)
+template <typename F>
+void for_each_line(const std::string& text, F&& fn) {
+    size_t pos = 0;
+    std::string line;
+    while (pos < text.size()) {
+        line.clear();
+        for (;;) {
+            size_t e = text.find('\n', pos);
+            size_t len = (e == std::string::npos ? text.size() : e) - pos;
+            line.append(text, pos, len);
+            pos = (e == std::string::npos) ? text.size() : e + 1;
+            if (!line.empty() && line.back() == '\\' && pos < text.size()) {
+                line.pop_back();
+                continue;
+            }
+            break;
+        }
+        fn(line);
+    }
+}
+
+int find_material(const ObjModel& m, const std::string& name) {   // ObjReader.hpp:78-88
+    for (size_t i = 1; i < m.materials.size(); ++i)
+        if (m.materials[i].name == name) return static_cast<int>(i);
+    return 0;
+}
+
+void read_mtl(ObjModel& m, const std::string& path) {   // ObjReader.cpp:163-259
+    const std::string text = slurp(path);
+    int idx = 0;
+    std::string tok;
+    for_each_line(text, [&](const std::string& line) {
+        Cursor c{line.data(), line.data() + line.size()};
+        if (!c.token(tok) || tok[0] == '#') return;
+        if (tok == "newmtl") {
+            c.token(tok);
+            idx = find_material(m, tok);
+            if (idx == 0) {
+                ObjMaterial mt;
+                mt.name = tok;
+                m.materials.push_back(mt);
+                idx = static_cast<int>(m.materials.size()) - 1;
+            }
+        } else if (tok == "Ka" || tok == "Kd" || tok == "Ks") {
+            Vec3 v;
+            v.x = c.number<float>();
+            v.y = c.number<float>();
+            v.z = c.number<float>();
+            ObjMaterial& mt = m.materials[idx];
+            if (tok[1] == 'a') mt.Ka = v;
+            else if (tok[1] == 'd') mt.Kd = v;
+            else { mt.Ks = v; mt.Ns = 2; }
+        } else if (tok == "Ns") {
+            m.materials[idx].Ns = c.number<double>();
+        } else if (tok == "Tr") {
+            m.materials[idx].Tr = c.number<double>();
+        } else if (tok == "Ni") {
+            m.materials[idx].Ni = c.number<double>();
+        }
+    });
+}
+
+}  // namespace
+
+void read_obj(const std::string& path, ObjModel& m) {   // ObjReader.cpp:8-161
+    m = ObjModel();
+    m.path = path;
+    m.vertices.push_back(Vec3{});
+    m.n_texcoords = 1;
+    m.normals.push_back(Vec3{});
+    m.triangles.push_back(ObjTriangle{});
+    m.materials.push_back(ObjMaterial{});
+    const std::string text = slurp(path);
+    std::vector<int32_t>* group = &m.groups["default"];
+    int material = 0;
+    std::string tok;
+    for_each_line(text, [&](const std::string& line) {
+        Cursor c{line.data(), line.data() + line.size()};
+        if (!c.token(tok) || tok[0] == '#') return;
+        if (tok == "v" || tok == "vn") {
+            Vec3 v;
+            v.x = c.number<float>();
+            v.y = c.number<float>();
+            v.z = c.number<float>();
+            (tok.size() == 1 ? m.vertices : m.normals).push_back(v);
+        } else if (tok == "f") {
+            int k = 0;
+            m.triangles.push_back(ObjTriangle{});
+            m.triangles.back().material = material;
+            group->push_back(static_cast<int32_t>(m.triangles.size() - 1));
+            std::string vt;
+            while (c.token(vt)) {
+                int32_t vi, ti, ni;
+                if (!parse_face_vertex(vt, vi, ti, ni)) throw Error{MCPT_E_PARSE, "Invalid OBJ file!"};
+                if (k < 3) {
+                    ObjTriangle& t = m.triangles.back();
+                    t.v[k] = vi; t.t[k] = ti; t.n[k] = ni;
+                } else {   // fan: (v0, previous v2, new)
+                    ObjTriangle nt;
+                    const ObjTriangle prev = m.triangles.back();
+                    nt.material = material;
+                    nt.v[0] = prev.v[0]; nt.v[1] = prev.v[2]; nt.v[2] = vi;
+                    nt.t[0] = prev.t[0]; nt.t[1] = prev.t[2]; nt.t[2] = ti;
+                    nt.n[0] = prev.n[0]; nt.n[1] = prev.n[2]; nt.n[2] = ni;
+                    m.triangles.push_back(nt);
+                    group->push_back(static_cast<int32_t>(m.triangles.size() - 1));
+                }
+                ++k;
+            }
+        } else if (tok == "vt") {
+            ++m.n_texcoords;
+        } else if (tok == "g") {
+            c.token(tok);   // on failure tok keeps "g"
+            group = &m.groups[tok];
+        } else if (tok == "usemtl") {
+            c.token(tok);
+            material = find_material(m, tok);
+        } else if (tok == "mtllib") {
+            c.token(tok);
+            size_t slash = path.find_last_of('/');
+            std::string dir = (slash == std::string::npos) ? std::string(".") : path.substr(0, slash);
+            read_mtl(m, dir + "/" + tok);
+        }
+    });
+}
+
+// ---------------------------------------------------------------------------
+void build_host_scene(const ObjModel& m, HostScene& hs) {
+    hs = HostScene();
+    const int64_t ntri = static_cast<int64_t>(m.triangles.size());
+    // CreateGeometry (CUTracer.cu:277-311): one record per non-empty group,
+    // start = first triangle index, material of that triangle.
+    for (const auto& kv : m.groups) {
+        const auto& ids = kv.second;
+        if (ids.empty()) continue;
+        const ObjMaterial& mt = m.materials[static_cast<size_t>(m.triangles[static_cast<size_t>(ids[0])].material)];
+        Geometry g;
+        g.Ka = mt.Ka; g.Kd = mt.Kd; g.Ks = mt.Ks;
+        g.Ns = static_cast<float>(mt.Ns);
+        g.Tr = static_cast<float>(mt.Tr);
+        g.Ni = static_cast<float>(mt.Ni);
+        g.start = static_cast<uint32_t>(ids[0]);
+        g.count = static_cast<uint32_t>(ids.size());
+        hs.geoms.push_back(g);
+    }
+    // the brute-force loop (CUTracer.cu:49-54) tests triangle start+i of each
+    // geometry in order: rank = position in that loop, geometry = first cover
+    std::vector<int32_t> geom_of(static_cast<size_t>(ntri), -1);
+    std::vector<uint32_t> rank_of(static_cast<size_t>(ntri), 0);
+    uint32_t rank = 0;
+    for (size_t g = 0; g < hs.geoms.size(); ++g) {
+        for (uint32_t i = 0; i < hs.geoms[g].count; ++i, ++rank) {
+            uint64_t cv = static_cast<uint64_t>(hs.geoms[g].start) + i;
+            if (cv >= static_cast<uint64_t>(ntri))
+                throw Error{MCPT_E_INVALID, "geometry range exceeds the triangle count"};
+            if (geom_of[cv] < 0) {
+                geom_of[cv] = static_cast<int32_t>(g);
+                rank_of[cv] = rank;
+            }
+        }
+    }
+    const int64_t nv = static_cast<int64_t>(m.vertices.size());
+    const int64_t nn = static_cast<int64_t>(m.normals.size());
+    for (int64_t i = 0; i < ntri; ++i) {
+        if (geom_of[static_cast<size_t>(i)] < 0) continue;
+        const ObjTriangle& t = m.triangles[static_cast<size_t>(i)];
+        for (int j = 0; j < 3; ++j)
+            if (t.v[j] < 0 || t.v[j] >= nv || t.n[j] < 0 || t.n[j] >= nn)
+                throw Error{MCPT_E_INVALID, "triangle " + std::to_string(i) + " has an out-of-range index"};
+        hs.kd_tris.push_back(static_cast<int32_t>(i));
+        hs.kd_geom.push_back(static_cast<uint32_t>(geom_of[static_cast<size_t>(i)]));
+        hs.kd_prio.push_back(rank_of[static_cast<size_t>(i)]);
+        for (int j = 0; j < 3; ++j) {
+            const Vec3& p = m.vertices[static_cast<size_t>(t.v[j])];
+            const Vec3& q = m.normals[static_cast<size_t>(t.n[j])];
+            hs.kd_verts.insert(hs.kd_verts.end(), {p.x, p.y, p.z});
+            hs.kd_normals.insert(hs.kd_normals.end(), {q.x, q.y, q.z});
+        }
+    }
+    build_kdtree(hs.kd_verts, hs.nodes, hs.leaf_ids, hs.kd_depth);
+}
+
+// ---------------------------------------------------------------------------
+// KD build (KDTree.hpp:58-287).  Literal std::min/std::max forms keep the
+// signed-zero/NaN behaviour of the reference; float expressions keep its
+// operand order (the library is compiled with -ffp-contract=off).
+namespace {
+
+inline float smin(float a, float b) { return (b < a) ? b : a; }
+inline float smax(float a, float b) { return (a < b) ? b : a; }
+
+struct Box {
+    float mn[3], mx[3];
+    static Box empty() {
+        Box b;
+        for (int i = 0; i < 3; ++i) { b.mn[i] = FLT_MAX; b.mx[i] = -FLT_MAX; }
+        return b;
+    }
+    void add_pt(const float* p) {
+        for (int i = 0; i < 3; ++i) { mn[i] = smin(mn[i], p[i]); mx[i] = smax(mx[i], p[i]); }
+    }
+    void add(const Box& r) { add_pt(r.mn); add_pt(r.mx); }
+    void clip(const Box& r) {
+        for (int i = 0; i < 3; ++i) { mn[i] = smax(mn[i], r.mn[i]); mx[i] = smin(mx[i], r.mx[i]); }
+    }
+    float half_area() const {
+        float s0 = mx[0] - mn[0], s1 = mx[1] - mn[1], s2 = mx[2] - mn[2];
+        return s0 * s1 + s1 * s2 + s2 * s0;
+    }
+};
+
+struct BNode {
+    Box box;
+    std::vector<uint32_t> ids;   // ascending (std::set<UINT>)
+    uint32_t axis = 0;
+    float split = 0.0f;
+    int32_t left = -1, right = -1;
+    int depth = 0;
+};
+
+// flat-on-plane -> left; min < v -> left; max > v -> right (KDTree.hpp:129-153)
+template <typename FL, typename FR>
+inline void classify(const Box& tb, int a, float v, FL&& to_left, FR&& to_right) {
+    if (tb.mn[a] == tb.mx[a] && tb.mn[a] == v) {
+        to_left();
+    } else {
+        if (tb.mn[a] < v) to_left();
+        if (tb.mx[a] > v) to_right();
+    }
+}
+
+}  // namespace
+
+void build_kdtree(const std::vector<float>& tv, std::vector<KdNode>& out,
+                  std::vector<uint32_t>& leaf_ids, int& depth_out) {
+    const size_t n = tv.size() / 9;
+    std::vector<Box> tbox(n);
+    for (size_t k = 0; k < n; ++k) {
+        tbox[k] = Box::empty();
+        for (int j = 0; j < 3; ++j) tbox[k].add_pt(&tv[9 * k + 3 * j]);
+    }
+    auto node_box = [&](const std::vector<uint32_t>& ids) {   // GetNodeAABB
+        Box b = Box::empty();
+        for (uint32_t id : ids) b.add(tbox[id]);
+        return b;
+    };
+
+    std::vector<BNode> nodes;
+    nodes.reserve(2 * n + 1);
+    nodes.emplace_back();
+    nodes[0].ids.resize(n);
+    std::iota(nodes[0].ids.begin(), nodes[0].ids.end(), 0u);
+    nodes[0].box = node_box(nodes[0].ids);
+    std::deque<int32_t> work{0};
+    int max_depth = 0;
+
+    struct Cand { float v; uint32_t ins; };
+    std::vector<Cand> cands;
+
+    while (!work.empty()) {
+        const int32_t ni = work.front();
+        work.pop_front();
+        const int depth = nodes[ni].depth;
+        max_depth = std::max(max_depth, depth);
+        if (depth >= 32) continue;
+        const Box box = nodes[ni].box;
+        const std::vector<uint32_t>& ids = nodes[ni].ids;
+        int ax = -1;
+        float val = 0.0f;
+        if (ids.size() > 64u) {
+            // spatial median of the longest axis (KDTree.hpp:108-122)
+            float sz[3] = {box.mx[0] - box.mn[0], box.mx[1] - box.mn[1], box.mx[2] - box.mn[2]};
+            ax = 0;
+            for (int i = 1; i < 3; ++i) if (sz[i] > sz[ax]) ax = i;
+            val = 0.5f * (box.mx[ax] + box.mn[ax]);
+        } else {
+            // SAH over vertex coordinates, Cts = 0 (KDTree.hpp:164-285)
+            const float A0 = box.half_area();
+            const float SAH0 = static_cast<float>(ids.size());
+            float minSAH = FLT_MAX;
+            for (int a = 0; a < 3; ++a) {
+                cands.clear();
+                for (uint32_t id : ids)
+                    for (int j = 0; j < 3; ++j)
+                        cands.push_back({tv[9 * id + 3 * j + a], static_cast<uint32_t>(cands.size())});
+                std::stable_sort(cands.begin(), cands.end(), [](const Cand& x, const Cand& y) { return x.v < y.v; });
+                for (size_t q = 0; q < cands.size(); ++q) {
+                    if (q > 0 && !(cands[q - 1].v < cands[q].v)) continue;   // std::set keeps the first
+                    const float v = cands[q].v;
+                    if (v < box.mn[a] || v > box.mx[a]) continue;
+                    unsigned numL = 0, numR = 0;
+                    Box bL = box, bR = box, tL = Box::empty(), tR = Box::empty();
+                    bL.mx[a] = v;
+                    bR.mn[a] = v;
+                    for (uint32_t id : ids)
+                        classify(tbox[id], a, v,
+                                 [&] { ++numL; tL.add(tbox[id]); },
+                                 [&] { ++numR; tR.add(tbox[id]); });
+                    bL.clip(tL);
+                    bR.clip(tR);
+                    const float AL = bL.half_area(), AR = bR.half_area();
+                    const float SAH = (AL * static_cast<float>(numL) + AR * static_cast<float>(numR)) / A0 + 0.0f;
+                    if (SAH < minSAH) { minSAH = SAH; ax = a; val = v; }
+                }
+            }
+            if (!(minSAH < SAH0)) ax = -1;
+        }
+        if (ax < 0) continue;   // leaf
+
+        BNode l, r;
+        l.box = box; l.box.mx[ax] = val;
+        r.box = box; r.box.mn[ax] = val;
+        for (uint32_t id : ids)
+            classify(tbox[id], ax, val, [&] { l.ids.push_back(id); }, [&] { r.ids.push_back(id); });
+        l.box.clip(node_box(l.ids));
+        r.box.clip(node_box(r.ids));
+        l.depth = r.depth = depth + 1;
+        nodes[ni].axis = static_cast<uint32_t>(ax + 1);
+        nodes[ni].split = val;
+        nodes[ni].left = static_cast<int32_t>(nodes.size());
+        nodes[ni].right = static_cast<int32_t>(nodes.size() + 1);
+        std::vector<uint32_t>().swap(nodes[ni].ids);
+        nodes.push_back(std::move(l));
+        nodes.push_back(std::move(r));
+        work.push_back(static_cast<int32_t>(nodes.size() - 2));
+        work.push_back(static_cast<int32_t>(nodes.size() - 1));
+    }
+
+    // BFS flatten: children of a node land at consecutive BFS indices
+    out.clear();
+    out.reserve(nodes.size());
+    leaf_ids.clear();
+    std::deque<int32_t> bfs{0};
+    while (!bfs.empty()) {
+        const BNode& b = nodes[static_cast<size_t>(bfs.front())];
+        bfs.pop_front();
+        KdNode o;
+        for (int i = 0; i < 3; ++i) { o.bmin[i] = b.box.mn[i]; o.bmax[i] = b.box.mx[i]; }
+        if (b.axis) {
+            o.left = static_cast<uint32_t>(out.size() + bfs.size() + 1);
+            o.right = o.left + 1;
+            o.axis = b.axis;
+            o.split = b.split;
+            bfs.push_back(b.left);
+            bfs.push_back(b.right);
+        } else {
+            o.leaf_begin = static_cast<uint32_t>(leaf_ids.size());
+            o.leaf_count = static_cast<uint32_t>(b.ids.size());
+            leaf_ids.insert(leaf_ids.end(), b.ids.begin(), b.ids.end());
+        }
+        out.push_back(o);
+    }
+    depth_out = max_depth;
+}
+
+}  // namespace mcpt

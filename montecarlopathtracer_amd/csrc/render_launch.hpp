@@ -1,0 +1,69 @@
+// render_launch.hpp -- device scene image layout and kernel parameters.
+//
+// Scene image (one contiguous device buffer, 16-byte aligned sections; the
+// same bytes are copied verbatim into LDS by the in-LDS kernel variant):
+//   tris   3 x float4 per KD triangle: (a.xyz, brute-force rank bits),
+//          (a-b .xyz, geometry index bits), (a-c .xyz, 0)       48 B
+//   nodes  uint2 per KD node (BFS): inner  x = axis<<30 | left child,
+//          y = split value bits; leaf x = 3<<30 | first leaf ref, y = count  8 B
+//   leafs  uint32 KD triangle id per leaf reference                    4 B
+//   geoms  GpuGeom per geometry (material of CUTracer.cu:300-308)      64 B
+// Shading normals live outside the image (read once per shaded hit):
+//   normals 3 x float4 per KD triangle (n0, n1, n2)                    48 B
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mcpt {
+
+constexpr int kLdsBlock = 1024;          // in-LDS variant: one 16-wave workgroup per CU
+constexpr int kGlobalBlock = 256;        // global variant
+constexpr int kGlobalBlocksPerCu = 4;
+constexpr size_t kMaxLds = 160 * 1024;   // gfx950 LDS per CU
+
+struct GpuGeom {
+    float Ka[3], Kd[3], Ks[3];
+    float Ns, Tr, Ni;
+    uint32_t Ns_u;                       // (PWuint)Ns, Utils.hpp:72 parameter type
+    uint32_t pad[3];
+};
+static_assert(sizeof(GpuGeom) == 64, "GpuGeom layout");
+
+struct GpuScene {
+    const unsigned char* image;
+    const float4* normals;
+    uint32_t image_bytes;
+    uint32_t off_tris, off_nodes, off_leafs, off_geoms;
+    uint32_t n_tris, n_nodes, n_leafs, n_geoms;
+    float root_min[3], root_max[3];
+};
+
+struct KernelParams {
+    GpuScene scene;
+    int32_t width, height;
+    int32_t tile, tiles_x, shard_count, shard_index, packed;
+    uint32_t npix_local;                 // owned tiles * tile^2
+    uint32_t spp, spp_offset, chunk, nchunks, total_units;
+    int32_t max_depth;
+    float illum, tan_half_fov;
+    int32_t fresnel_kd;
+    uint32_t prev_count;
+    float eye[3], fwd[3], up[3], right[3];
+    uint32_t key;                        // TEA-16 key of the 64-bit seed
+    float4* partial;                     // [nchunks][npix_local]
+    uint32_t* counter;                   // work-unit counter
+    unsigned long long* stats;           // 8 counters
+    uint4* spill;                        // traversal-stack spill [32][total_lanes]
+    uint32_t total_lanes;
+    uint32_t lds_stack_off;              // LDS offset of the stack arrays
+    uint32_t* unit_counters;             // optional [total_units][4]: rays, inner, leaf, tests
+};
+
+size_t lds_bytes_in_lds(uint32_t image_bytes, int S);
+int total_lanes_for(uint32_t image_bytes, int cus);
+// memset counter, path kernel (events ev0/ev1 around it), reduce kernel (ev2)
+hipError_t launch_render(const KernelParams& kp, int cus, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1,
+                         hipEvent_t ev2, float4* fb, int* variant_out);
+
+}  // namespace mcpt

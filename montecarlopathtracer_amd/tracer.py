@@ -1,0 +1,319 @@
+"""Host-side mirror of the reference tracer interface, over the C ABI.
+
+Reference interface (pw1316/MonteCarloPathTracer, CVMCTracer/CVMCTracer):
+  PW::FileReader::ObjModel::readObj(path)        Framework/ObjReader.hpp:55
+  PW::Tracer::Initialize()                       CUDA/CUTracer.h:9
+  PW::Tracer::CreateGeometry(const ObjModel*)    CUDA/CUTracer.h:10
+  PW::Tracer::DestroyGeometry()                  CUDA/CUTracer.h:11
+  PW::Tracer::RenderScene(sceneID, hostcolor)    CUDA/CUTracer.h:12
+and its only caller, main.cpp:16-18 / 33-35.
+
+Same names, argument meaning and call order.  Differences:
+  * errors raise McptError instead of returning a mostly-ignored cudaError_t;
+  * the scene is held by a Tracer object (module functions keep one default
+    Tracer, like the reference's module globals);
+  * RenderScene keeps the reference's progressive loop (NUM_KERNELS launches of
+    NUM_SAMPLES_PER_KERNEL samples, running mean with prevCount, CUTracer.cu:
+    378-398) but without the OpenCV window/PNG side effects.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _capi
+from ._capi import McptError, RenderParamsC, RenderStats, check, lib
+
+# CV/stdafx.h:41-46
+IMG_WIDTH = 800
+IMG_HEIGHT = 600
+NUM_KERNELS = 100
+NUM_SAMPLES_PER_KERNEL = 100
+ILLUM = 10.0
+DEFAULT_SEED = 0x4D435054
+
+
+def _fptr(a):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+class ObjModel:
+    """PW::FileReader::ObjModel (ObjReader.hpp:37-63): OBJ/MTL data with dummy index 0."""
+
+    def __init__(self, path: Optional[str] = None):
+        self._h = None
+        self.path = None
+        if path is not None:
+            self.read_obj(path)
+
+    def read_obj(self, path: str) -> bool:   # ObjModel::readObj (ObjReader.cpp:8)
+        h = C.c_void_p()
+        check(lib().mcpt_model_read_obj(path.encode(), C.byref(h)))
+        self._free()
+        self._h = h
+        self.path = path
+        return True
+
+    readObj = read_obj
+
+    def _free(self):
+        if self._h is not None and _capi._lib is not None:
+            _capi._lib.mcpt_model_free(self._h)
+        self._h = None
+
+    def __del__(self):
+        self._free()
+
+    @property
+    def handle(self):
+        if self._h is None:
+            raise McptError(-1, "model not loaded")
+        return self._h
+
+    def info(self) -> dict:
+        i = _capi.ModelInfo()
+        check(lib().mcpt_model_get_info(self.handle, C.byref(i)))
+        return {n: int(getattr(i, n)) for n, _ in i._fields_}
+
+    def vertices(self) -> np.ndarray:
+        a = np.zeros((self.info()["n_vertices"], 3), np.float32)
+        check(lib().mcpt_model_copy_vertices(self.handle, _fptr(a)))
+        return a
+
+    def normals(self) -> np.ndarray:
+        a = np.zeros((self.info()["n_normals"], 3), np.float32)
+        check(lib().mcpt_model_copy_normals(self.handle, _fptr(a)))
+        return a
+
+    def triangles(self) -> np.ndarray:
+        """(n, 10) int32: vertex[3], texture[3], normal[3], material index."""
+        a = np.zeros((self.info()["n_triangles"], 10), np.int32)
+        check(lib().mcpt_model_copy_triangles(self.handle, a.ctypes.data_as(C.POINTER(C.c_int32))))
+        return a
+
+    def materials(self) -> np.ndarray:
+        """(n, 12) float64: Ka[3] Kd[3] Ks[3] Ns Tr Ni."""
+        a = np.zeros((self.info()["n_materials"], 12), np.float64)
+        check(lib().mcpt_model_copy_materials(self.handle, a.ctypes.data_as(C.POINTER(C.c_double))))
+        return a
+
+    def groups(self) -> dict:
+        out = {}
+        buf = C.create_string_buffer(1024)
+        for g in range(self.info()["n_groups"]):
+            n = C.c_int64()
+            check(lib().mcpt_model_group(self.handle, g, buf, 1024, C.byref(n), None))
+            a = np.zeros(n.value, np.int32)
+            check(lib().mcpt_model_group(self.handle, g, buf, 1024, C.byref(n),
+                                         a.ctypes.data_as(C.POINTER(C.c_int32))))
+            out[buf.value.decode()] = a
+        return out
+
+
+@dataclass
+class RenderParams:
+    """Render configuration; defaults are the CVMCTracer constants for scene 1."""
+    width: int = IMG_WIDTH
+    height: int = IMG_HEIGHT
+    spp: int = NUM_SAMPLES_PER_KERNEL
+    spp_offset: int = 0
+    spp_chunk: int = 32               # summation chunk (part of the result definition)
+    max_depth: int = 7                # CUTracer.cu:212
+    illum: float = ILLUM
+    fov_deg: float = 60.0             # CUTracer.cu:189
+    eye: Sequence[float] = (0.0, 5.0, 17.0)
+    direction: Sequence[float] = (0.0, 0.0, -1.0)
+    up: Sequence[float] = (0.0, 1.0, 0.0)
+    seed: int = DEFAULT_SEED
+    prev_count: int = 0
+    fresnel_kd: bool = True
+    tile: int = 8
+    shard_count: int = 1
+    shard_index: int = 0
+    packed: bool = False
+
+    @staticmethod
+    def for_scene(scene_id: int, **kw) -> "RenderParams":
+        """Camera of RenderScene(sceneID) (CUTracer.cu:347-374)."""
+        eye = (0.0, 5.0, 17.0) if scene_id == 1 else (0.0, 5.0, 23.0)
+        return RenderParams(eye=eye, **kw)
+
+    def to_c(self) -> RenderParamsC:
+        p = RenderParamsC()
+        p.width, p.height = int(self.width), int(self.height)
+        p.spp, p.spp_offset, p.spp_chunk = int(self.spp), int(self.spp_offset), int(self.spp_chunk)
+        p.max_depth, p.illum, p.fov_deg = int(self.max_depth), float(self.illum), float(self.fov_deg)
+        p.eye[:] = [float(x) for x in self.eye]
+        p.dir[:] = [float(x) for x in self.direction]
+        p.up[:] = [float(x) for x in self.up]
+        p.seed = int(self.seed) & 0xFFFFFFFFFFFFFFFF
+        p.prev_count = int(self.prev_count)
+        p.fresnel_kd = 1 if self.fresnel_kd else 0
+        p.tile, p.shard_count, p.shard_index = int(self.tile), int(self.shard_count), int(self.shard_index)
+        p.packed = 1 if self.packed else 0
+        return p
+
+    def output_pixels(self) -> int:
+        if self.packed or self.shard_count > 1:
+            return int(lib().mcpt_shard_pixel_count(C.byref(self.to_c())))
+        return int(self.width) * int(self.height)
+
+    def shard_pixels(self) -> np.ndarray:
+        """(n, 2) int32 (x, y) of every output slot of a packed/sharded render (-1 = padding)."""
+        p = self.to_c()
+        n = int(check(lib().mcpt_shard_pixel_count(C.byref(p))))
+        xy = np.zeros((n, 2), np.int32)
+        check(lib().mcpt_shard_pixels(C.byref(p), xy.ctypes.data_as(C.POINTER(C.c_int32))))
+        return xy
+
+
+class Scene:
+    """A device-resident scene (CreateGeometry result + KD tree)."""
+
+    def __init__(self, model: ObjModel, host_only: bool = False):
+        h = C.c_void_p()
+        fn = lib().mcpt_scene_create_host if host_only else lib().mcpt_scene_create
+        check(fn(model.handle, C.byref(h)))
+        self._h = h
+        self.host_only = host_only
+
+    def close(self):
+        if self._h is not None and _capi._lib is not None:
+            _capi._lib.mcpt_scene_destroy(self._h)
+        self._h = None
+
+    __del__ = close
+
+    @property
+    def handle(self):
+        if self._h is None:
+            raise McptError(-1, "scene destroyed")
+        return self._h
+
+    def info(self) -> dict:
+        i = _capi.SceneInfo()
+        check(lib().mcpt_scene_get_info(self.handle, C.byref(i)))
+        return {n: int(getattr(i, n)) for n, _ in i._fields_}
+
+    def kd(self):
+        """(nodes (n,12) u32, leaf ids, kd_tris, geoms (g,14) f32) as built."""
+        i = self.info()
+        nodes = np.zeros((i["n_nodes"], 12), np.uint32)
+        leafs = np.zeros(max(i["n_leaf_refs"], 1), np.uint32)
+        kdt = np.zeros(i["n_triangles"], np.int32)
+        geoms = np.zeros((i["n_geometries"], 14), np.float32)
+        check(lib().mcpt_scene_copy_kd(self.handle, nodes.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                       leafs.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                       kdt.ctypes.data_as(C.POINTER(C.c_int32)), _fptr(geoms)))
+        return nodes, leafs[: i["n_leaf_refs"]], kdt, geoms
+
+    def render(self, params: RenderParams, fb: Optional[np.ndarray] = None):
+        """Synchronous render into a host float32 RGB buffer; returns (fb, stats)."""
+        n = params.output_pixels()
+        if fb is None:
+            fb = np.zeros((n, 3) if (params.packed or params.shard_count > 1) else (params.height, params.width, 3),
+                          np.float32)
+        if fb.dtype != np.float32 or not fb.flags.c_contiguous or fb.size != 3 * n:
+            raise McptError(-1, "fb must be a C-contiguous float32 array with 3 floats per output pixel")
+        st = RenderStats()
+        check(lib().mcpt_render(self.handle, C.byref(params.to_c()), _fptr(fb), C.byref(st)))
+        return fb, st.as_dict()
+
+    def render_unit_counters(self, params: RenderParams):
+        """Synchronous render returning (fb, per-unit counters (units, 4): rays, inner, leaf, tests)."""
+        n = params.output_pixels()
+        fb = np.zeros((n, 3), np.float32)
+        chunk = params.spp_chunk if 0 < params.spp_chunk < params.spp else params.spp
+        units = n * ((params.spp + chunk - 1) // chunk)
+        uc = np.zeros((units, 4), np.uint32)
+        check(lib().mcpt_render_unit_counters(self.handle, C.byref(params.to_c()), _fptr(fb),
+                                              uc.ctypes.data_as(C.POINTER(C.c_uint32))))
+        return fb, uc
+
+    def render_device(self, params: RenderParams, d_fb_rgba_ptr: int, stream_ptr: int = 0):
+        """Asynchronous render into a device RGBA float buffer (e.g. a torch tensor's data_ptr())."""
+        check(lib().mcpt_render_device(self.handle, C.byref(params.to_c()), C.c_void_p(d_fb_rgba_ptr),
+                                       C.c_void_p(stream_ptr)))
+
+    def reserve(self, params: RenderParams):
+        check(lib().mcpt_scene_reserve(self.handle, C.byref(params.to_c())))
+
+    def stats(self) -> dict:
+        st = RenderStats()
+        check(lib().mcpt_render_stats_read(self.handle, C.byref(st)))
+        return st.as_dict()
+
+
+class Tracer:
+    """PW::Tracer as an object: Initialize / CreateGeometry / DestroyGeometry / RenderScene."""
+
+    def __init__(self):
+        self.scene: Optional[Scene] = None
+        self.last_stats: dict = {}
+
+    def initialize(self, devices: Sequence[int] = (0,)) -> int:   # CUTracer.cu:220-223 (cudaSetDevice(0))
+        arr = (C.c_int32 * len(devices))(*devices)
+        return check(lib().mcpt_init(arr, len(devices)))
+
+    def create_geometry(self, model: ObjModel) -> int:             # CUTracer.cu:225-314
+        self.destroy_geometry()
+        self.scene = Scene(model)
+        return 0
+
+    def destroy_geometry(self) -> int:                              # CUTracer.cu:316-338
+        if self.scene is not None:
+            self.scene.close()
+            self.scene = None
+        return 0
+
+    def render_scene(self, scene_id: int, hostcolor: np.ndarray, num_kernels: int = NUM_KERNELS,
+                     samples_per_kernel: int = NUM_SAMPLES_PER_KERNEL, callback=None, **kw) -> int:
+        """RenderScene (CUTracer.cu:340-404): num_kernels launches of samples_per_kernel
+        samples; after launch k the buffer holds the running mean (prevCount = k)."""
+        if self.scene is None:
+            raise McptError(-1, "CreateGeometry has not been called")
+        H, W = hostcolor.shape[:2]
+        stats = {}
+        for each in range(num_kernels):
+            p = RenderParams.for_scene(scene_id, width=W, height=H, spp=samples_per_kernel,
+                                       spp_offset=each * samples_per_kernel, prev_count=each, **kw)
+            _, st = self.scene.render(p, hostcolor)
+            for k, v in st.items():
+                stats[k] = stats.get(k, 0) + v if k != "variant" else v
+            if callback is not None:
+                callback(each, hostcolor)
+        self.last_stats = stats
+        return 0
+
+    # reference spellings
+    Initialize = initialize
+    CreateGeometry = create_geometry
+    DestroyGeometry = destroy_geometry
+    RenderScene = render_scene
+
+
+_default = Tracer()
+
+
+def Initialize() -> int:
+    return _default.initialize()
+
+
+def CreateGeometry(model: ObjModel) -> int:
+    return _default.create_geometry(model)
+
+
+def DestroyGeometry() -> int:
+    return _default.destroy_geometry()
+
+
+def RenderScene(sceneID: int, hostcolor: np.ndarray, **kw) -> int:
+    return _default.render_scene(sceneID, hostcolor, **kw)
+
+
+def encode_8bit(hostcolor: np.ndarray) -> np.ndarray:
+    """8-bit RGB as main.cpp:19-29 writes it: value*255 saturated, no gamma."""
+    return np.clip(hostcolor * 255.0, 0, 255).astype(np.uint8)
