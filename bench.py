@@ -1,0 +1,202 @@
+#!/usr/bin/env python3
+"""bench.py -- Cornell Box 1024x1024 @ 1024 spp on N MI355X (BASELINE.json configs[1]/[2]).
+
+One step = one full path-traced frame of the workload (every pixel, every
+sample, up to 7 scatter events + 1 terminal query per path) through the C ABI
+(mcpt_render_device), plus -- for N > 1 -- the RCCL gather of the per-rank
+tile buffers to rank 0 and its unpermute into the image.  Pixels are sharded
+as interleaved 8x8 tiles (tile t -> rank t % N); total work is fixed, so the
+scaling is strong.  value = closest-hit queries of all ranks / max-over-ranks
+wall time (Mray/s).
+
+Launch:  python bench.py [--gpus 1 --steps 3 --warmup 1]
+         python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+             --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Mray/s + achieved HBM GB/s, Cornell Box 1024spp at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def algorithmic_bytes(st: dict, pixels: int) -> dict:
+    """B_ray = 32*N_node + 4*N_leafref + 48*N_tri + 96*N_shade, + 16 B per pixel.
+    'own' = the same counts priced with this kernel's records (8-B KD nodes)."""
+    nodes = st["inner_visits"] + st["leaf_visits"]
+    survey = 32 * nodes + 4 * st["leaf_refs"] + 48 * st["tri_tests"] + 96 * st["shades"] + 16 * pixels
+    own = 8 * nodes + 4 * st["leaf_refs"] + 48 * st["tri_tests"] + 96 * st["shades"] + 16 * pixels
+    return {"survey": survey, "own": own}
+
+
+def cpu_baseline(scene_name: str, width: int, height: int, seconds: float) -> dict:
+    """Reference CPU path = the oracle (C restatement of CUTracer.cu + the reference
+    KD traversal rtx.hlsl:84-211), single thread, on a bounded centred crop."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # test/bench infrastructure only
+    from montecarlopathtracer_amd.scenes import scene_path
+    oracle.build()
+    s = oracle.Scene(scene_path(scene_name))
+    crop = 64
+    spp = 8
+    total_rays, total_t = 0, 0.0
+    runs = 0
+    while total_t < seconds and runs < 64:
+        x0 = (width - crop) // 2 + (runs % 4) * 8
+        y0 = (height - crop) // 2 + (runs // 4 % 4) * 8
+        p = oracle.RenderParams(width=width, height=height, spp=spp, spp_chunk=32, spp_offset=runs * spp,
+                                traversal=oracle.KD_REF, threads=1, region=(x0, y0, x0 + crop, y0 + crop))
+        t0 = time.perf_counter()
+        _, c = s.render(p)
+        total_t += time.perf_counter() - t0
+        total_rays += c["rays"]
+        runs += 1
+    return {"value": round(total_rays / total_t / 1e6, 4), "unit": "Mray/s", "cores": 1, "kind": "port",
+            "sample": f"{runs} x ({crop}x{crop} centred crop, {spp} spp) of {scene_name} {width}x{height}, "
+                      f"{total_rays} rays in {total_t:.1f}s, oracle traversal=KD_REF (rtx.hlsl order), 1 thread"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scene", default="scene01")
+    ap.add_argument("--width", type=int, default=1024)
+    ap.add_argument("--height", type=int, default=1024)
+    ap.add_argument("--spp", type=int, default=1024)
+    ap.add_argument("--spp-chunk", type=int, default=32)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import montecarlopathtracer_amd as M
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local if world > 1 else 0)
+    torch.cuda.set_device(dev)
+    M.Tracer().initialize([dev.index])
+
+    scene = M.Scene(M.ObjModel(M.scene_path(args.scene)))
+    scene_id = 1 if args.scene == "scene01" else 2
+    p = M.RenderParams.for_scene(scene_id, width=args.width, height=args.height, spp=args.spp,
+                                 spp_chunk=args.spp_chunk, tile=8, shard_count=world, shard_index=rank,
+                                 packed=world > 1)
+    n_out = p.output_pixels()
+    fb = torch.zeros((n_out, 4), dtype=torch.float32, device=dev)
+    scene.reserve(p)
+    stream = torch.cuda.current_stream(dev)
+
+    if world > 1:
+        # gather buffers + the (x, y) of every slot of every rank, for the unpermute
+        counts = [M.RenderParams(width=args.width, height=args.height, tile=8, shard_count=world,
+                                 shard_index=r).output_pixels() for r in range(world)]
+        maxn = max(counts)
+        send = torch.zeros((maxn, 4), dtype=torch.float32, device=dev)
+        gather = [torch.zeros((maxn, 4), dtype=torch.float32, device=dev) for _ in range(world)] if rank == 0 else None
+        image = torch.zeros((args.height * args.width, 4), dtype=torch.float32, device=dev) if rank == 0 else None
+        if rank == 0:
+            idx, valid = [], []
+            for r in range(world):
+                xy = M.RenderParams(width=args.width, height=args.height, tile=8, shard_count=world,
+                                    shard_index=r).shard_pixels()
+                xy_t = torch.from_numpy(xy).to(dev)
+                ok = xy_t[:, 0] >= 0
+                idx.append((xy_t[:, 1] * args.width + xy_t[:, 0])[ok])
+                valid.append(ok)
+
+    def step():
+        scene.render_device(p, fb.data_ptr(), stream.cuda_stream)
+        if world > 1:
+            send[:n_out].copy_(fb)
+            dist.gather(send, gather, dst=0)
+            if rank == 0:
+                for r in range(world):
+                    image[idx[r]] = gather[r][:counts[r]][valid[r]]
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    scene.stats()   # reset counters/timers after warmup
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    st = scene.stats()   # waits for the recorded HIP events of each path-kernel launch
+
+    rays = st["rays"]
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        agg = torch.tensor([st[k] for k in ("rays", "paths", "inner_visits", "leaf_visits", "leaf_refs",
+                                              "tri_tests", "shades")] + [st["kernel_ms"]],
+                           dtype=torch.float64, device=dev)
+        dist.all_reduce(agg, op=dist.ReduceOp.SUM)
+        rays = int(agg[0].item())
+
+    if rank == 0:
+        per_launch = {k: st[k] / max(st["renders"], 1) for k in
+                      ("rays", "inner_visits", "leaf_visits", "leaf_refs", "tri_tests", "shades")}
+        kern_ms = st["kernel_ms"] / max(st["renders"], 1)
+        ab = algorithmic_bytes(per_launch, n_out)
+        achieved = ab["survey"] / (kern_ms * 1e-3) / 1e9
+        achieved_own = ab["own"] / (kern_ms * 1e-3) / 1e9
+        mray = rays / elapsed / 1e6
+        line = {
+            "metric": METRIC, "value": round(mray, 3), "unit": "Mray/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+            "data": f"bundled reference scene {args.scene}.obj (Cornell Box), synthetic camera/seed",
+            "config": {"workload": f"cornell_{args.width}x{args.height}_{args.spp}spp", "scene": args.scene,
+                       "width": args.width, "height": args.height, "spp": args.spp, "max_depth": 7,
+                       "spp_chunk": args.spp_chunk, "parallelism": f"pixel-tiles x{world}" +
+                       (" + rccl gather" if world > 1 else ""), "kernel_variant": st["variant"]},
+            "rays_per_step": rays // args.steps,
+            "rays_per_path": round(st["rays"] / max(st["paths"], 1), 4),
+            "kernel_ms_avg": round(kern_ms, 3),
+            "gpu_ms_per_step_event": round(ev0.elapsed_time(ev1) / args.steps, 3),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "bytes_model": "SURVEY 8(d): 32*nodes+4*leafrefs+48*tris+96*shades+16*px",
+                         "achieved_own_layout": round(achieved_own, 1),
+                         "bytes_per_ray": round(ab["survey"] / max(per_launch["rays"], 1), 1),
+                         "per_ray": {k: round(per_launch[k] / max(per_launch["rays"], 1), 3) for k in
+                                     ("inner_visits", "leaf_visits", "leaf_refs", "tri_tests", "shades")}},
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(args.scene, args.width, args.height, args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -10,6 +10,7 @@
 #include <cfloat>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -238,6 +239,11 @@ Plan make_plan(const mcpt_scene& s, const mcpt_render_params* p) {
     k.up[0] = u.x; k.up[1] = u.y; k.up[2] = u.z;
     k.right[0] = r.x; k.right[1] = r.y; k.right[2] = r.z;
     k.key = tea16(static_cast<uint32_t>(p->seed), static_cast<uint32_t>(p->seed >> 32));
+    {
+        const char* e = std::getenv("MCPT_READY_THRESH");
+        const int th = e ? std::atoi(e) : 32;
+        k.ready_thresh = th < 1 ? 1 : (th > 64 ? 64 : th);
+    }
     pl.out_pixels = k.packed ? size_t(npix) : size_t(p->width) * size_t(p->height);
     return pl;
 }

@@ -31,12 +31,6 @@ using namespace dev;
 
 namespace {
 
-struct Hit {
-    int32_t tri;
-    float beta, gamma;
-    V3 hp;
-};
-
 struct Counters {
     uint32_t rays, paths, inner, leaf, refs, tests, shades, spills;
 };
@@ -45,124 +39,153 @@ __device__ __forceinline__ float sel3(int a, float x, float y, float z) {
     return a == 0 ? x : (a == 1 ? y : z);
 }
 
-// Ordered KD traversal; mirrors oracle/render_ref.c isect_kd_ordered().
-template <int S>
-__device__ __forceinline__ Hit trace(V3 o, V3 d, const GpuScene& sc, const float4* __restrict__ tris,
-                                     const uint2* __restrict__ nodes, const uint32_t* __restrict__ leafs,
-                                     uint32_t* st_node, float* st_lo, float* st_hi, int stride,
-                                     uint4* __restrict__ spill, uint32_t spill_stride, Counters& c) {
-    Hit h;
-    h.tri = -1;
-    h.beta = h.gamma = 0.0f;
-    h.hp = v3(0.0f, 0.0f, 0.0f);
-    const float ix = 1.0f / d.x, iy = 1.0f / d.y, iz = 1.0f / d.z;
+// lane modes of the persistent loop
+constexpr int kDead = 0;    // no more work
+constexpr int kTrav = 1;    // traversing its current ray
+constexpr int kReady = 2;   // closest hit known, waiting for a shading round
+constexpr int kNeed = 3;    // needs a work unit
+
+// Per-lane ray + traversal state.  The traversal is the ordered front-to-back
+// KD walk of oracle/render_ref.c isect_kd_ordered(), split into resumable
+// iterations (descend to a leaf, test its triangles, pop).
+struct RayState {
+    V3 o, d;
+    float ix, iy, iz;
+    float tmin, tmax, best;
+    uint32_t node, bprio;
+    int32_t sp, htri;
+    float hbeta, hgamma;
+};
+
+// root interval (oracle: isect_kd_ordered prologue); returns false on a miss
+__device__ __forceinline__ bool begin_ray(RayState& r, const GpuScene& sc) {
+    r.ix = 1.0f / r.d.x;
+    r.iy = 1.0f / r.d.y;
+    r.iz = 1.0f / r.d.z;
+    r.htri = -1;
+    r.hbeta = r.hgamma = 0.0f;
+    r.best = kFltMax;
+    r.bprio = 0xFFFFFFFFu;
+    r.node = 0;
+    r.sp = 0;
     float tmin = 0.0f, tmax = kFltMax;
-    {
-        const float oo[3] = {o.x, o.y, o.z}, dd[3] = {d.x, d.y, d.z}, inv[3] = {ix, iy, iz};
+    const float oo[3] = {r.o.x, r.o.y, r.o.z}, dd[3] = {r.d.x, r.d.y, r.d.z}, inv[3] = {r.ix, r.iy, r.iz};
+    bool miss = false;
 #pragma unroll
-        for (int a = 0; a < 3; a++) {
-            if (dd[a] == 0.0f) {
-                if (oo[a] < sc.root_min[a] || oo[a] > sc.root_max[a]) return h;
-            } else {
-                float t0 = (sc.root_min[a] - oo[a]) * inv[a];
-                float t1 = (sc.root_max[a] - oo[a]) * inv[a];
-                float lo = dd[a] < 0.0f ? t1 : t0;
-                float hi = dd[a] < 0.0f ? t0 : t1;
-                tmin = lo > tmin ? lo : tmin;
-                tmax = hi < tmax ? hi : tmax;
-            }
+    for (int a = 0; a < 3; a++) {
+        if (dd[a] == 0.0f) {
+            miss = miss || (oo[a] < sc.root_min[a] || oo[a] > sc.root_max[a]);
+        } else {
+            const float t0 = (sc.root_min[a] - oo[a]) * inv[a];
+            const float t1 = (sc.root_max[a] - oo[a]) * inv[a];
+            const float lo = dd[a] < 0.0f ? t1 : t0;
+            const float hi = dd[a] < 0.0f ? t0 : t1;
+            tmin = lo > tmin ? lo : tmin;
+            tmax = hi < tmax ? hi : tmax;
         }
     }
-    if (tmin > tmax * kEpsHi) return h;
+    r.tmin = tmin;
+    r.tmax = tmax;
+    return !miss && !(tmin > tmax * kEpsHi);
+}
 
-    float best = kFltMax;
-    uint32_t bprio = 0xFFFFFFFFu;
-    uint32_t node = 0;
-    int sp = 0;
-
-    auto push = [&](uint32_t n, float lo, float hi) {
-        const int slot = (sp & (S - 1)) * stride;
-        if (sp >= S) {
-            spill[(uint32_t)(sp - S) * spill_stride] = make_uint4(st_node[slot], __float_as_uint(st_lo[slot]),
-                                                                  __float_as_uint(st_hi[slot]), 0u);
-            c.spills++;
+// Cramer test (CUTracer.cu:54-92) with an exact-result-preserving prefilter:
+// the three IEEE divisions run only when the signs of the determinants allow
+// beta, gamma, t > 0 and the magnitudes do not already rule out beta+gamma < 1
+// or t < best (2^-20 margins cover every rounding of the exact path).
+__device__ __forceinline__ void test_tri(RayState& r, const float4* __restrict__ tris, uint32_t k) {
+    const float4 A0 = tris[3 * k], A1 = tris[3 * k + 1], A2 = tris[3 * k + 2];
+    const float aox = A0.x - r.o.x, aoy = A0.y - r.o.y, aoz = A0.z - r.o.z;
+    const float detA = det3(A1.x, A2.x, r.d.x, A1.y, A2.y, r.d.y, A1.z, A2.z, r.d.z);
+    const float qb = det3(aox, A2.x, r.d.x, aoy, A2.y, r.d.y, aoz, A2.z, r.d.z);
+    const float qg = det3(A1.x, aox, r.d.x, A1.y, aoy, r.d.y, A1.z, aoz, r.d.z);
+    const float qt = det3(A1.x, A2.x, aox, A1.y, A2.y, aoy, A1.z, A2.z, aoz);
+    const uint32_t sA = __float_as_uint(detA) & 0x80000000u;
+    const bool signs_ok = ((__float_as_uint(qb) & 0x80000000u) == sA) & ((__float_as_uint(qg) & 0x80000000u) == sA) &
+                          ((__float_as_uint(qt) & 0x80000000u) == sA) & (qb != 0.0f) & (qg != 0.0f) &
+                          (qt != 0.0f) & (detA != 0.0f);
+    const float adet = fabsf(detA) * 1.00000095367431640625f;   // 1 + 2^-20
+    const bool mags_ok = !(fabsf(qb) + fabsf(qg) > adet) & !(fabsf(qt) > r.best * adet);
+    if (signs_ok & mags_ok) {
+        const float beta = qb / detA;
+        const float gamma = qg / detA;
+        const float t = qt / detA;
+        const uint32_t prio = __float_as_uint(A0.w);
+        if (beta + gamma < 1.0f && beta > 0.0f && gamma > 0.0f && t > 0.0f &&
+            (t < r.best || (t == r.best && prio < r.bprio))) {
+            r.best = t;
+            r.bprio = prio;
+            r.htri = (int32_t)k;
+            r.hbeta = beta;
+            r.hgamma = gamma;
         }
-        st_node[slot] = n;
-        st_lo[slot] = lo;
-        st_hi[slot] = hi;
-        sp++;
-    };
-
-    for (;;) {
-        uint2 nd = nodes[node];
-        while ((nd.x >> 30) != 3u) {
-            c.inner++;
-            const int a = (int)(nd.x >> 30);
-            const float sv = __uint_as_float(nd.y);
-            const uint32_t left = nd.x & 0x3FFFFFFFu;
-            const float oa = sel3(a, o.x, o.y, o.z);
-            const float da = sel3(a, d.x, d.y, d.z);
-            const float ia = sel3(a, ix, iy, iz);
-            const float t = (sv - oa) * ia;
-            const bool below = (oa < sv) || (oa == sv && da <= 0.0f);
-            const uint32_t nearc = below ? left : left + 1;
-            const uint32_t farc = below ? left + 1 : left;
-            if (da == 0.0f && oa == sv) {
-                push(farc, tmin, tmax);
-                node = nearc;
-            } else if (!(t > 0.0f) || t > tmax * kEpsHi) {
-                node = nearc;
-            } else if (t * kEpsHi < tmin) {
-                node = farc;
-            } else {
-                push(farc, t > tmin ? t : tmin, tmax);
-                node = nearc;
-                tmax = t < tmax ? t : tmax;
-            }
-            nd = nodes[node];
-        }
-        c.leaf++;
-        const uint32_t begin = nd.x & 0x3FFFFFFFu;
-        const uint32_t cnt = nd.y;
-        for (uint32_t i = 0; i < cnt; i++) {
-            const uint32_t k = leafs[begin + i];
-            c.refs++;
-            c.tests++;
-            const float4 A0 = tris[3 * k], A1 = tris[3 * k + 1], A2 = tris[3 * k + 2];
-            // a, e1 = a-b, e2 = a-c (exact precomputed differences)
-            const float aox = A0.x - o.x, aoy = A0.y - o.y, aoz = A0.z - o.z;
-            const float detA = det3(A1.x, A2.x, d.x, A1.y, A2.y, d.y, A1.z, A2.z, d.z);
-            const float beta = det3(aox, A2.x, d.x, aoy, A2.y, d.y, aoz, A2.z, d.z) / detA;
-            const float gamma = det3(A1.x, aox, d.x, A1.y, aoy, d.y, A1.z, aoz, d.z) / detA;
-            const float t = det3(A1.x, A2.x, aox, A1.y, A2.y, aoy, A1.z, A2.z, aoz) / detA;
-            const uint32_t prio = __float_as_uint(A0.w);
-            if (beta + gamma < 1.0f && beta > 0.0f && gamma > 0.0f && t > 0.0f &&
-                (t < best || (t == best && prio < bprio))) {
-                best = t;
-                bprio = prio;
-                h.tri = (int32_t)k;
-                h.beta = beta;
-                h.gamma = gamma;
-                h.hp = v3(o.x + t * d.x, o.y + t * d.y, o.z + t * d.z);
-            }
-        }
-        if (sp == 0) break;
-        sp--;
-        {
-            const int slot = (sp & (S - 1)) * stride;
-            node = st_node[slot];
-            tmin = st_lo[slot];
-            tmax = st_hi[slot];
-            if (sp >= S) {
-                const uint4 e = spill[(uint32_t)(sp - S) * spill_stride];
-                st_node[slot] = e.x;
-                st_lo[slot] = __uint_as_float(e.y);
-                st_hi[slot] = __uint_as_float(e.z);
-            }
-        }
-        if (best <= tmin * kEpsLo) break;
     }
-    return h;
+}
+
+// One resumable traversal iteration: descend to a leaf, test it, pop.
+// Returns true when the ray's closest hit is final.
+template <int S>
+__device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict__ tris,
+                                          const uint2* __restrict__ nodes, const uint32_t* __restrict__ leafs,
+                                          uint32_t* st_node, float* st_lo, float* st_hi, int stride,
+                                          uint4* __restrict__ spill, uint32_t spill_stride, Counters& c) {
+    uint2 nd = nodes[r.node];
+    while ((nd.x >> 30) != 3u) {
+        c.inner++;
+        const int a = (int)(nd.x >> 30);
+        const float sv = __uint_as_float(nd.y);
+        const uint32_t left = nd.x & 0x3FFFFFFFu;
+        const float oa = sel3(a, r.o.x, r.o.y, r.o.z);
+        const float da = sel3(a, r.d.x, r.d.y, r.d.z);
+        const float ia = sel3(a, r.ix, r.iy, r.iz);
+        const float t = (sv - oa) * ia;
+        const bool below = (oa < sv) || (oa == sv && da <= 0.0f);
+        const uint32_t nearc = below ? left : left + 1;
+        const uint32_t farc = below ? left + 1 : left;
+        // if/else chain of the oracle, evaluated branch-free
+        const bool pp = (da == 0.0f) & (oa == sv);                  // ray inside the plane: both
+        const bool no = !(t > 0.0f) | (t > r.tmax * kEpsHi);        // near child only
+        const bool fo = t * kEpsHi < r.tmin;                        // far child only
+        const bool go_far = !pp & !no & fo;
+        const bool push_it = pp | (!no & !fo);
+        if (push_it) {
+            const float plo = pp ? r.tmin : (t > r.tmin ? t : r.tmin);
+            const int slot = (r.sp & (S - 1)) * stride;
+            if (r.sp >= S) {
+                spill[(uint32_t)(r.sp - S) * spill_stride] = make_uint4(st_node[slot], __float_as_uint(st_lo[slot]),
+                                                                        __float_as_uint(st_hi[slot]), 0u);
+                c.spills++;
+            }
+            st_node[slot] = farc;
+            st_lo[slot] = plo;
+            st_hi[slot] = r.tmax;
+            r.sp++;
+            if (!pp) r.tmax = t < r.tmax ? t : r.tmax;
+        }
+        r.node = go_far ? farc : nearc;
+        nd = nodes[r.node];
+    }
+    c.leaf++;
+    const uint32_t begin = nd.x & 0x3FFFFFFFu;
+    const uint32_t cnt = nd.y;
+    for (uint32_t i = 0; i < cnt; i++) {
+        c.refs++;
+        c.tests++;
+        test_tri(r, tris, leafs[begin + i]);
+    }
+    if (r.sp == 0) return true;
+    r.sp--;
+    const int slot = (r.sp & (S - 1)) * stride;
+    r.node = st_node[slot];
+    r.tmin = st_lo[slot];
+    r.tmax = st_hi[slot];
+    if (r.sp >= S) {
+        const uint4 e = spill[(uint32_t)(r.sp - S) * spill_stride];
+        st_node[slot] = e.x;
+        st_lo[slot] = __uint_as_float(e.y);
+        st_hi[slot] = __uint_as_float(e.z);
+    }
+    return r.best <= r.tmin * kEpsLo;
 }
 
 // work unit v (packed owned-pixel index) -> image pixel; false outside the image
@@ -177,7 +200,26 @@ __device__ __forceinline__ bool unit_pixel(const KernelParams& kp, uint32_t v, i
     return x < kp.width && y < kp.height;
 }
 
-template <bool IN_LDS, int S, int BLOCK>
+// primary ray of sample s of pixel (px, py) (CUTracer.cu:186-211)
+__device__ __forceinline__ void primary_ray(const KernelParams& kp, uint32_t pix, int px, int py, uint32_t s,
+                                            uint32_t& sd, V3& dir) {
+    sd = rng_init(pix, kp.key, kp.spp_offset + s);
+    const float biasx = (float)(uint32_t)px + (rng_next(sd) * 2.0f - 1.0f);
+    const float biasy = (float)(uint32_t)py + (rng_next(sd) * 2.0f - 1.0f);
+    const double th = (double)kp.tan_half_fov;
+    const double W = (double)(uint32_t)kp.width, H = (double)(uint32_t)kp.height;
+    const float idx = (float)((2.0 * (double)biasx / W - 1) * th);
+    const float idy = (float)((1.0 * H / W - 2.0 * (double)biasy / W) * th);
+    const float idz = -1.0f;
+    V3 wr;
+    wr.x = kp.right[0] * idx + kp.up[0] * idy - kp.fwd[0] * idz;
+    wr.y = kp.right[1] * idx + kp.up[1] * idy - kp.fwd[1] * idz;
+    wr.z = kp.right[2] * idx + kp.up[2] * idy - kp.fwd[2] * idz;
+    normalize_cu(wr);
+    dir = wr;
+}
+
+template <bool IN_LDS, int S, int BLOCK, bool DBG>
 __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = (int)threadIdx.x;
@@ -211,94 +253,83 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
     const uint32_t gl = blockIdx.x * BLOCK + (uint32_t)tid;
     uint4* spill = kp.spill + gl;
     const uint32_t spill_stride = kp.total_lanes;
-
     const V3 eye = v3(kp.eye[0], kp.eye[1], kp.eye[2]);
-    const V3 fwd = v3(kp.fwd[0], kp.fwd[1], kp.fwd[2]);
-    const V3 up = v3(kp.up[0], kp.up[1], kp.up[2]);
-    const V3 right = v3(kp.right[0], kp.right[1], kp.right[2]);
 
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0};
-    bool alive = true, has_unit = false, need_path = false;
-    uint32_t s = 0, s_end = 0, pix = 0, v = 0, chunk = 0, unit_id = 0;
-    Counters c0 = c;
+    Counters c0 = c;   // DBG builds only
+    int mode = kNeed;
+    uint32_t s = 0, s_end = 0, unit_id = 0;
     int px = 0, py = 0, depth = 0;
     uint32_t sd = 1;
-    V3 part = v3(0, 0, 0), color = v3(1, 1, 1), o = eye, dir = v3(0, 0, -1);
+    V3 part = v3(0, 0, 0), color = v3(1, 1, 1);
+    RayState r;
+    r.o = eye;
+    r.d = v3(0, 0, -1);
+    r.htri = -1;
+
+    // start sample s of the current unit: primary ray, then its root interval
+    auto start_path = [&]() {
+        const uint32_t pix = (uint32_t)py * (uint32_t)kp.width + (uint32_t)px;
+        primary_ray(kp, pix, px, py, s, sd, r.d);
+        r.o = eye;
+        color = v3(1, 1, 1);
+        depth = 0;
+        c.paths++;
+        c.rays++;
+        mode = begin_ray(r, sc) ? kTrav : kReady;
+    };
 
     for (;;) {
-        // ---- 1. refill work units: one atomic per wave ----------------------
-        const bool need_unit = alive && !has_unit;
-        const uint64_t m = __ballot(need_unit);
-        if (m) {
+        // ---- work units: one atomic per wave for every lane that needs one ----
+        for (;;) {
+            const uint64_t m = __ballot(mode == kNeed);
+            if (!m) break;
             const int leader = __ffsll((unsigned long long)m) - 1;
             uint32_t base = 0;
             if (lane == leader) base = atomicAdd(kp.counter, (uint32_t)__popcll(m));
             base = __shfl(base, leader);
-            if (need_unit) {
+            if (mode == kNeed) {
                 const uint32_t unit = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
                 if (unit >= kp.total_units) {
-                    alive = false;
+                    mode = kDead;
                 } else {
                     unit_id = unit;
-                    c0 = c;
-                    chunk = unit / kp.npix_local;
-                    v = unit - chunk * kp.npix_local;
+                    if constexpr (DBG) c0 = c;
+                    const uint32_t chunk = unit / kp.npix_local;
+                    const uint32_t v = unit - chunk * kp.npix_local;
                     s = chunk * kp.chunk;
                     s_end = min(s + kp.chunk, kp.spp);
                     part = v3(0, 0, 0);
                     if (unit_pixel(kp, v, px, py)) {
-                        pix = (uint32_t)py * (uint32_t)kp.width + (uint32_t)px;
-                        has_unit = true;
-                        need_path = true;
+                        start_path();
                     } else {
-                        kp.partial[(size_t)chunk * kp.npix_local + v] = make_float4(0, 0, 0, 0);
+                        kp.partial[unit] = make_float4(0, 0, 0, 0);
                     }
                 }
             }
         }
-        if (!__any(alive)) break;
+        if (!__ballot(mode != kDead)) break;
 
-        // ---- 2. new path: primary ray (CUTracer.cu:193-211) ---------------------
-        if (alive && has_unit && need_path) {
-            sd = rng_init(pix, kp.key, kp.spp_offset + s);
-            const float biasx = (float)(uint32_t)px + (rng_next(sd) * 2.0f - 1.0f);
-            const float biasy = (float)(uint32_t)py + (rng_next(sd) * 2.0f - 1.0f);
-            const double th = (double)kp.tan_half_fov;
-            const double W = (double)(uint32_t)kp.width, H = (double)(uint32_t)kp.height;
-            const float idx = (float)((2.0 * (double)biasx / W - 1) * th);
-            const float idy = (float)((1.0 * H / W - 2.0 * (double)biasy / W) * th);
-            const float idz = -1.0f;
-            V3 wr;
-            wr.x = right.x * idx + up.x * idy - fwd.x * idz;
-            wr.y = right.y * idx + up.y * idy - fwd.y * idz;
-            wr.z = right.z * idx + up.z * idy - fwd.z * idz;
-            normalize_cu(wr);
-            o = eye;
-            dir = wr;
-            color = v3(1, 1, 1);
-            depth = 0;
-            need_path = false;
-            c.paths++;
-        }
-        const bool tracing = alive && has_unit;
-
-        // ---- 3. closest hit -------------------------------------------------
-        Hit h;
-        h.tri = -1;
-        if (tracing) {
-            c.rays++;
-            h = trace<S>(o, dir, sc, tris, nodes, leafs, st_node, st_lo, st_hi, BLOCK, spill, spill_stride, c);
+        // ---- traversal burst: until half the wave is ready to shade --------
+        for (;;) {
+            if (mode == kTrav) {
+                if (trav_iter<S>(r, tris, nodes, leafs, st_node, st_lo, st_hi, BLOCK, spill, spill_stride, c))
+                    mode = kReady;
+            }
+            const uint64_t trv = __ballot(mode == kTrav);
+            const uint64_t rdy = __ballot(mode == kReady);
+            if (!trv || __popcll(rdy) >= kp.ready_thresh) break;
         }
 
-        // ---- 4. shade (CUTracer.cu:105-175) ---------------------------------
-        if (tracing) {
+        // ---- shading round for every ready lane (CUTracer.cu:105-175) -------
+        if (mode == kReady) {
             bool done = false;
             V3 L = v3(0, 0, 0);
             if (depth < kp.max_depth) {
-                if (h.tri < 0) {
+                if (r.htri < 0) {
                     done = true;
                 } else {
-                    const uint32_t gi = __float_as_uint(tris[3 * h.tri + 1].w);
+                    const uint32_t gi = __float_as_uint(tris[3 * r.htri + 1].w);
                     const GpuGeom& g = geoms[gi];
                     if (g.Ka[0] > 0 || g.Ka[1] > 0 || g.Ka[2] > 0) {
                         L = v3(color.x * (g.Ka[0] * kp.illum), color.y * (g.Ka[1] * kp.illum),
@@ -306,12 +337,13 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
                         done = true;
                     } else {
                         c.shades++;
-                        const float4 n1 = sc.normals[3 * h.tri], n2 = sc.normals[3 * h.tri + 1],
-                                     n3 = sc.normals[3 * h.tri + 2];
-                        V3 nrm = vadd(vadd(vscale(v3(n1.x, n1.y, n1.z), 1.0f - h.beta - h.gamma),
-                                           vscale(v3(n2.x, n2.y, n2.z), h.beta)),
-                                      vscale(v3(n3.x, n3.y, n3.z), h.gamma));
+                        const float4 n1 = sc.normals[3 * r.htri], n2 = sc.normals[3 * r.htri + 1],
+                                     n3 = sc.normals[3 * r.htri + 2];
+                        V3 nrm = vadd(vadd(vscale(v3(n1.x, n1.y, n1.z), 1.0f - r.hbeta - r.hgamma),
+                                           vscale(v3(n2.x, n2.y, n2.z), r.hbeta)),
+                                      vscale(v3(n3.x, n3.y, n3.z), r.hgamma));
                         normalize_cu(nrm);
+                        V3 dir = r.d;
                         if (g.Tr > 0) {
                             dir = sample_fresnel(sd, nrm, dir, g.Tr, g.Ni);
                             if (kp.fresnel_kd) color = v3(color.x * g.Kd[0], color.y * g.Kd[1], color.z * g.Kd[2]);
@@ -327,13 +359,19 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
                                 dir = sample_hemi(sd, nrm);
                             }
                         }
-                        o = vadd(h.hp, vscale(dir, 0.01f));
+                        // hitPoint = pos + t*dir at the accepted t (CUTracer.cu:89-91), then
+                        // pos = hitPoint + dir*0.01 (:134,143,159)
+                        const V3 hp = v3(r.o.x + r.best * r.d.x, r.o.y + r.best * r.d.y, r.o.z + r.best * r.d.z);
+                        r.o = vadd(hp, vscale(dir, 0.01f));
+                        r.d = dir;
                         depth++;
+                        c.rays++;
+                        mode = begin_ray(r, sc) ? kTrav : kReady;
                     }
                 }
             } else {
-                if (h.tri >= 0) {
-                    const uint32_t gi = __float_as_uint(tris[3 * h.tri + 1].w);
+                if (r.htri >= 0) {
+                    const uint32_t gi = __float_as_uint(tris[3 * r.htri + 1].w);
                     const GpuGeom& g = geoms[gi];
                     L = v3(color.x * (g.Ka[0] * kp.illum), color.y * (g.Ka[1] * kp.illum),
                            color.z * (g.Ka[2] * kp.illum));
@@ -344,17 +382,17 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
                 part = vadd(part, L);
                 s++;
                 if (s == s_end) {
-                    kp.partial[(size_t)chunk * kp.npix_local + v] = make_float4(part.x, part.y, part.z, 0.0f);
-                    has_unit = false;
-                    if (kp.unit_counters) {
+                    kp.partial[unit_id] = make_float4(part.x, part.y, part.z, 0.0f);   // [chunk][v]
+                    if constexpr (DBG) {
                         uint32_t* uc = kp.unit_counters + 4 * (size_t)unit_id;
                         uc[0] = c.rays - c0.rays;
                         uc[1] = c.inner - c0.inner;
                         uc[2] = c.leaf - c0.leaf;
                         uc[3] = c.tests - c0.tests;
                     }
+                    mode = kNeed;
                 } else {
-                    need_path = true;
+                    start_path();
                 }
             }
         }
@@ -401,7 +439,7 @@ __global__ void __launch_bounds__(256) reduce_kernel(const KernelParams kp, floa
 
 template <bool IN_LDS, int S, int BLOCK>
 hipError_t launch_path(const KernelParams& kp, int grid, size_t lds, hipStream_t st) {
-    auto kern = path_kernel<IN_LDS, S, BLOCK>;
+    auto kern = kp.unit_counters ? path_kernel<IN_LDS, S, BLOCK, true> : path_kernel<IN_LDS, S, BLOCK, false>;
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;

@@ -58,6 +58,7 @@ struct KernelParams {
     uint32_t total_lanes;
     uint32_t lds_stack_off;              // LDS offset of the stack arrays
     uint32_t* unit_counters;             // optional [total_units][4]: rays, inner, leaf, tests
+    int32_t ready_thresh;                // lanes ready before a shading round (1..64)
 };
 
 size_t lds_bytes_in_lds(uint32_t image_bytes, int S);
