@@ -102,32 +102,15 @@ def main():
     scene.reserve(p)
     stream = torch.cuda.current_stream(dev)
 
+    gatherer = None
     if world > 1:
-        # gather buffers + the (x, y) of every slot of every rank, for the unpermute
-        counts = [M.RenderParams(width=args.width, height=args.height, tile=8, shard_count=world,
-                                 shard_index=r).output_pixels() for r in range(world)]
-        maxn = max(counts)
-        send = torch.zeros((maxn, 4), dtype=torch.float32, device=dev)
-        gather = [torch.zeros((maxn, 4), dtype=torch.float32, device=dev) for _ in range(world)] if rank == 0 else None
-        image = torch.zeros((args.height * args.width, 4), dtype=torch.float32, device=dev) if rank == 0 else None
-        if rank == 0:
-            idx, valid = [], []
-            for r in range(world):
-                xy = M.RenderParams(width=args.width, height=args.height, tile=8, shard_count=world,
-                                    shard_index=r).shard_pixels()
-                xy_t = torch.from_numpy(xy).to(dev)
-                ok = xy_t[:, 0] >= 0
-                idx.append((xy_t[:, 1] * args.width + xy_t[:, 0])[ok])
-                valid.append(ok)
+        from montecarlopathtracer_amd.sharding import TileGather
+        gatherer = TileGather(args.width, args.height, world, rank, dev, tile=8)
 
     def step():
         scene.render_device(p, fb.data_ptr(), stream.cuda_stream)
-        if world > 1:
-            send[:n_out].copy_(fb)
-            dist.gather(send, gather, dst=0)
-            if rank == 0:
-                for r in range(world):
-                    image[idx[r]] = gather[r][:counts[r]][valid[r]]
+        if gatherer is not None:
+            gatherer.gather(fb)   # RCCL gather of the packed tile buffers + unpermute on rank 0
 
     for _ in range(args.warmup):
         step()
@@ -180,6 +163,7 @@ def main():
                        (" + rccl gather" if world > 1 else ""), "kernel_variant": st["variant"]},
             "rays_per_step": rays // args.steps,
             "rays_per_path": round(st["rays"] / max(st["paths"], 1), 4),
+            "stack_spills_per_ray": round(st["stack_spills"] / max(st["rays"], 1), 4),
             "kernel_ms_avg": round(kern_ms, 3),
             "gpu_ms_per_step_event": round(ev0.elapsed_time(ev1) / args.steps, 3),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -1,0 +1,61 @@
+"""Pixel-tile sharding across GPUs and the tile gather to rank 0.
+
+The image is cut into tile x tile pixel tiles; tile t belongs to rank
+t % world (interleaved, so every rank gets a similar mix of the bright floor,
+the spheres and the ~20% black miss region).  Each rank renders its tiles
+packed (mcpt_render_params.packed) into a (n_local, 4) float buffer; rank 0
+gathers every rank's buffer with one torch.distributed.gather (RCCL over xGMI
+on MI355X, gloo on CPU) and scatters the slots back to image order.
+
+There is no reference counterpart: the reference renders on one device
+(CUTracer.cu:220-223 selects device 0).
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import numpy as np
+
+from .tracer import RenderParams
+
+
+def shard_params(base: RenderParams, world: int, rank: int, tile: int = 8) -> RenderParams:
+    """Copy of base restricted to rank's tiles, written packed."""
+    import dataclasses
+    return dataclasses.replace(base, tile=tile, shard_count=world, shard_index=rank, packed=world > 1)
+
+
+class TileGather:
+    """Gathers packed per-rank tile buffers into one row-major (H*W, 4) image on rank 0."""
+
+    def __init__(self, width: int, height: int, world: int, rank: int, device, tile: int = 8):
+        import torch
+        self.width, self.height, self.world, self.rank, self.tile = width, height, world, rank, tile
+        probe = [RenderParams(width=width, height=height, tile=tile, shard_count=world, shard_index=r)
+                 for r in range(world)]
+        self.counts: List[int] = [p.output_pixels() for p in probe]
+        self.maxn = max(self.counts)
+        self.n_local = self.counts[rank]
+        self.send = torch.zeros((self.maxn, 4), dtype=torch.float32, device=device)
+        self.recv = None
+        self.image = None
+        if rank == 0:
+            self.recv = [torch.zeros((self.maxn, 4), dtype=torch.float32, device=device) for _ in range(world)]
+            self.image = torch.zeros((height * width, 4), dtype=torch.float32, device=device)
+            self.idx, self.valid = [], []
+            for r in range(world):
+                xy = torch.from_numpy(probe[r].shard_pixels().astype(np.int64)).to(device)
+                ok = xy[:, 0] >= 0
+                self.idx.append((xy[:, 1] * width + xy[:, 0])[ok])
+                self.valid.append(ok)
+
+    def gather(self, fb_local) -> Optional["torch.Tensor"]:
+        """fb_local: (n_local, 4) packed tiles of this rank. Returns the image on rank 0, None elsewhere."""
+        import torch.distributed as dist
+        self.send[: self.n_local].copy_(fb_local[: self.n_local])
+        dist.gather(self.send, self.recv if self.rank == 0 else None, dst=0)
+        if self.rank != 0:
+            return None
+        for r in range(self.world):
+            self.image[self.idx[r]] = self.recv[r][: self.counts[r]][self.valid[r]]
+        return self.image

@@ -1,0 +1,176 @@
+"""Product host code (libmcpt.so, no GPU calls): OBJ/MTL reader and KD build.
+
+* reader vs the reference's own tinyobjloader v1.1.1 (fixtures made by
+  tests/golden/make_golden.py from oracle/_ref/tinyobj_dump, which is built from
+  the reference header where it lies);
+* reader, CreateGeometry tables and KD tree vs the oracle restatement,
+  element for element / node for node, on the bundled scenes and on synthetic
+  edge cases (ngons, v//n forms, missing names, unknown materials, coplanar and
+  degenerate triangles, duplicated triangles, >64-triangle flat nodes).
+"""
+import os
+
+import numpy as np
+import pytest
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+SCENES = ["scene01", "scene02", "scene03"]
+
+
+@pytest.mark.parametrize("name", SCENES)
+def test_reader_matches_reference_tinyobjloader(mcpt, name):
+    g = np.load(os.path.join(GOLDEN, f"{name}_tinyobj.npz"))
+    m = mcpt.ObjModel(mcpt.scene_path(name))
+    v, n, t = m.vertices(), m.normals(), m.triangles()
+    # tinyobjloader parses numbers with its own routine: equal up to one float ulp
+    assert v.shape[0] - 1 == g["vertices"].shape[0] and n.shape[0] - 1 == g["normals"].shape[0]
+    assert np.allclose(v[1:], g["vertices"], rtol=2e-7, atol=1e-12)
+    assert np.allclose(n[1:], g["normals"], rtol=2e-7, atol=1e-12)
+    idx = g["indices"].reshape(-1, 3, 3)          # per face: 3 x (v, t, n), 0-based
+    assert t.shape[0] - 1 == idx.shape[0]
+    assert np.array_equal(t[1:, 0:3] - 1, idx[:, :, 0])
+    assert np.array_equal(t[1:, 6:9] - 1, idx[:, :, 2])
+    # faces per non-empty group == faces per tinyobj shape (same names)
+    groups = {k: len(a) for k, a in m.groups().items() if len(a)}
+    assert groups == dict(zip(g["shape_names"].tolist(), g["shape_faces"].tolist()))
+
+
+@pytest.mark.parametrize("name", SCENES)
+def test_reader_geometry_kd_match_oracle(mcpt, oracle_mod, name):
+    path = mcpt.scene_path(name)
+    _assert_same(mcpt, oracle_mod, path)
+
+
+def _assert_same(mcpt, oracle_mod, path):
+    m = mcpt.ObjModel(path)
+    o = oracle_mod.Scene(path)
+    assert np.array_equal(m.vertices(), o.vertices())
+    assert np.array_equal(m.normals(), o.normals())
+    assert np.array_equal(m.triangles()[1:], o.triangles()[1:])
+    assert np.array_equal(m.materials(), o.materials())
+    mg, og = m.groups(), o.groups()
+    assert list(mg) == list(og) and all(np.array_equal(mg[k], og[k]) for k in mg)
+    s = mcpt.Scene(m, host_only=True)
+    nodes, leafs, kdt, geoms = s.kd()
+    assert np.array_equal(geoms, o.geoms())
+    assert np.array_equal(kdt, o.kd_tris())
+    assert np.array_equal(nodes, o.kd_nodes())
+    assert np.array_equal(leafs, o.kd_leaf_ids())
+    info = s.info()
+    assert info["kd_depth"] == o.kd_depth and info["n_nodes"] == o.nnodes
+    return s
+
+
+def _write(tmp_path, obj, mtl):
+    (tmp_path / "t.mtl").write_text(mtl)
+    p = tmp_path / "t.obj"
+    p.write_text(obj)
+    return str(p)
+
+
+MTL = """newmtl light
+Kd 0.8 0.8 0.8
+Ka 0.78 0.78 0.78
+newmtl gloss
+Ks 1 1 1
+Ns 50
+newmtl glass
+Kd 0.5 0.5 0.5
+Tr 0.9
+Ni 1.5
+newmtl gloss
+Kd 0.1 0.2 0.3
+newmtl only_ks
+Ns 7
+Ks 0.5 0.5 0.5
+"""
+
+
+def test_reader_edge_cases_match_oracle(mcpt, oracle_mod, tmp_path):
+    obj = """# comment
+mtllib t.mtl
+v 0 0 0
+v 1 0 0
+v 1 1 0
+v 0 1 0
+v 0.5 0.5 -0.000000
+vn 0 0 1
+vn 0 0 -1
+vt 0 0
+g
+usemtl light
+f 1//1 2//1 3//1 4//1
+g quad
+usemtl gloss
+f 1/1/2 2/1/2 3/1/2 4/1/2 5/1/2
+usemtl nosuch
+f 1 2 \\
+ 3
+g quad
+usemtl only_ks
+f 2/1 3/1 5/1
+g default
+usemtl glass
+f 4 5 1
+"""
+    path = _write(tmp_path, obj, MTL)
+    _assert_same(mcpt, oracle_mod, path)
+    m = mcpt.ObjModel(path)
+    t = m.triangles()
+    assert t.shape[0] == 1 + 2 + 3 + 1 + 1 + 1                  # fan triangulation
+    assert list(t[2, 0:3]) == [1, 3, 4] and list(t[5, 0:3]) == [1, 4, 5]
+    assert "g" in m.groups()                                     # "g" with no name keeps the token
+    mats = m.materials()
+    names_ns = {round(x, 3) for x in mats[:, 9]}
+    assert 2.0 in names_ns and 7.0 not in names_ns               # Ks after Ns resets Ns to 2
+    assert t[6, 9] == 0                                          # unknown usemtl -> material 0
+
+
+def test_reader_errors(mcpt, tmp_path):
+    with pytest.raises(mcpt.McptError) as e:
+        mcpt.ObjModel(str(tmp_path / "missing.obj"))
+    assert e.value.code == -2
+    bad = _write(tmp_path, "v 0 0 0\nf 1/x 1 1\n", "")
+    with pytest.raises(mcpt.McptError) as e:
+        mcpt.ObjModel(bad)
+    assert e.value.code == -3
+    nomtl = tmp_path / "n.obj"
+    nomtl.write_text("mtllib none.mtl\n")
+    with pytest.raises(mcpt.McptError) as e:
+        mcpt.ObjModel(str(nomtl))
+    assert e.value.code == -2
+
+
+def _soup_obj(tris):
+    lines = []
+    for k, t in enumerate(tris):
+        for p in t:
+            lines.append("v %.9g %.9g %.9g" % tuple(p))
+    lines.append("vn 0 1 0")
+    lines.append("g soup")
+    for k in range(len(tris)):
+        lines.append("f %d//1 %d//1 %d//1" % (3 * k + 1, 3 * k + 2, 3 * k + 3))
+    return "\n".join(lines) + "\n"
+
+
+@pytest.mark.parametrize("kind", ["random", "flat", "mixed", "tiny"])
+def test_kd_build_synthetic_matches_oracle(mcpt, oracle_mod, tmp_path, kind):
+    r = np.random.default_rng({"random": 1, "flat": 2, "mixed": 3, "tiny": 4}[kind])
+    if kind == "random":
+        c = r.uniform(-5, 5, (400, 1, 3))
+        tris = c + r.normal(0, 0.6, (400, 3, 3))
+    elif kind == "flat":                     # >64 coplanar triangles: on-plane rule, flat nodes
+        c = r.uniform(-5, 5, (150, 1, 3)); c[..., 1] = 0
+        tris = c + r.normal(0, 0.5, (150, 3, 3)); tris[..., 1] = 0.0
+    elif kind == "mixed":                    # degenerate + duplicated + axis-aligned
+        c = r.uniform(-5, 5, (120, 1, 3))
+        tris = c + r.normal(0, 0.4, (120, 3, 3))
+        tris[:10] = tris[:10, :1]            # points
+        tris[10:20, 2] = tris[10:20, 1]      # segments
+        tris = np.concatenate([tris, tris[30:50]])
+        tris[60:80, :, 0] = np.round(tris[60:80, :, 0])
+    else:
+        tris = np.array([[[0, 0, 0], [1, 0, 0], [0, 1, 0]]], float)
+    path = _write(tmp_path, _soup_obj(tris.astype(np.float32)), "")
+    s = _assert_same(mcpt, oracle_mod, path)
+    assert s.info()["n_triangles"] == len(tris)

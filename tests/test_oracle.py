@@ -1,0 +1,181 @@
+"""The CPU oracle (test infrastructure) pinned against what the reference's own
+code and renders say.
+
+Pins used:
+  * KD-tree statistics of the reference's compiled KDTree.hpp build, recorded at
+    survey time: node/leaf counts, max leaf, depth;
+  * closest-hit equality of every KD mode with the brute-force restatement of
+    CUTracer.cu:44-96 (the reference's own semantic: 'same closest hit');
+  * the known answer sampleHemi(n=(0,1,0), u=(.25,.5)) = (-0.5, 0.8660254,
+    -4.37e-8) from the reference's Utils.hpp compiled with injected uniforms
+    (SURVEY.md §8(c));
+  * the reference's own render CV/result1.png (1000 spp), statistically.
+"""
+import os
+
+import numpy as np
+import pytest
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+# SURVEY.md §8(a) A3 (compiled reference KD build): nodes, leaves, max leaf, mean leaf, depth
+KD_REF_STATS = {
+    "scene01": dict(nodes=4395, leaves=2198, max_leaf=6, mean_leaf=1.86, depth=20),
+    "scene02": dict(nodes=7947, depth=32),
+    "scene03": dict(nodes=39201, max_leaf=13, depth=32),
+}
+
+
+@pytest.fixture(scope="module")
+def scenes(oracle_mod):
+    from montecarlopathtracer_amd.scenes import scene_path
+    return {k: oracle_mod.Scene(scene_path(k)) for k in ("scene01", "scene02", "scene03")}
+
+
+@pytest.mark.parametrize("name", ["scene01", "scene02", "scene03"])
+def test_kd_build_matches_reference_statistics(scenes, name):
+    s = scenes[name]
+    ref = KD_REF_STATS[name]
+    nodes = s.kd_nodes()
+    leaves = nodes[nodes[:, 2] == 0]
+    assert s.nnodes == ref["nodes"]
+    assert s.kd_depth == ref["depth"]
+    if "leaves" in ref:
+        assert len(leaves) == ref["leaves"]
+    if "max_leaf" in ref:
+        assert leaves[:, 11].max() == ref["max_leaf"]
+    if "mean_leaf" in ref:
+        assert abs(leaves[:, 11].mean() - ref["mean_leaf"]) < 0.005
+
+
+def test_scene_counts_match_survey(scenes):
+    s = scenes["scene01"]   # SURVEY.md §8(a) A1 (compiled reference reader)
+    assert (s.nverts, s.nnormals, s.ntris, s.nmats) == (441, 469, 863, 7)
+    assert {k: len(v) for k, v in s.groups().items()} == {
+        "default": 0, "pCube2": 12, "pSphere1": 420, "pSphere2": 420, "pWall1": 6, "pWall2": 2, "pWall3": 2}
+    assert scenes["scene02"].ntris == 1733 and scenes["scene03"].ntris == 3025
+
+
+@pytest.mark.parametrize("name", ["scene01", "scene03"])
+def test_kd_traversals_equal_brute_force(scenes, oracle_mod, name):
+    s = scenes[name]
+    r = np.random.default_rng(7)
+    n = 4000
+    nodes = s.kd_nodes()
+    bmin, bmax = nodes[0, 4:7].view(np.float32), nodes[0, 7:10].view(np.float32)
+    o = (bmin + (bmax - bmin) * r.random((n, 3))).astype(np.float32)
+    d = r.standard_normal((n, 3)).astype(np.float32)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    d[:50, 1] = 0.0                      # axis-parallel rays exercise the dir==0 paths
+    tb, gb, hb, _ = s.intersect(o, d, oracle_mod.BRUTE)
+    assert (tb >= 0).mean() > 0.5
+    for mode in (oracle_mod.KD_REF, oracle_mod.KD_ORDERED):
+        tk, gk, hk, c = s.intersect(o, d, mode)
+        assert np.array_equal(tb, tk) and np.array_equal(gb, gk)
+        assert np.array_equal(hb.view(np.uint32), hk.view(np.uint32))
+        assert c["tri_tests"] < 0.05 * n * s.nkd
+
+
+def test_render_modes_identical(scenes, oracle_mod):
+    s = scenes["scene01"]
+    imgs = []
+    for mode in (oracle_mod.BRUTE, oracle_mod.KD_REF, oracle_mod.KD_ORDERED):
+        img, c = s.render(oracle_mod.RenderParams(width=24, height=18, spp=2, traversal=mode, threads=4))
+        imgs.append(img)
+    assert np.array_equal(imgs[0], imgs[1]) and np.array_equal(imgs[0], imgs[2])
+
+
+def test_oracle_regression_fixture(scenes, oracle_mod):
+    g = np.load(os.path.join(GOLDEN, "oracle_scene01_32x24.npz"))
+    img, c = scenes["scene01"].render(oracle_mod.RenderParams(width=32, height=24, spp=4, spp_chunk=2,
+                                                              traversal=oracle_mod.KD_ORDERED, threads=4))
+    assert np.array_equal(img, g["image"])
+    assert [c["rays"], c["paths"], c["shades"]] == g["counters"].tolist()
+
+
+def test_sample_hemi_known_answer(oracle_mod):
+    import ctypes as C
+    L = oracle_mod.lib()
+    n = (C.c_float * 3)(0.0, 1.0, 0.0)
+    u = (C.c_float * 2)(0.25, 0.5)
+    out = (C.c_float * 3)()
+    L.orc_sample_hemi(n, u, out)
+    assert np.allclose(list(out), [-0.5, 0.8660254, -4.37e-8], rtol=0, atol=5e-8)   # survey printed 7 digits
+
+
+def test_samplers_rotate_into_normal_frame(oracle_mod):
+    import ctypes as C
+    L = oracle_mod.lib()
+    r = np.random.default_rng(3)
+    for _ in range(200):
+        nv = r.standard_normal(3).astype(np.float32)
+        nv /= np.linalg.norm(nv)
+        u = r.random(2).astype(np.float32)
+        out = (C.c_float * 3)()
+        L.orc_sample_hemi((C.c_float * 3)(*nv), (C.c_float * 2)(*u), out)
+        w = np.array(out)
+        # unit and in the upper hemisphere, up to the reference formula's own rounding:
+        # 1/sqrt(1 - n.y^2) (Utils.hpp:63) amplifies float error near the poles
+        tol = 1e-5 / max(1.0 - abs(float(nv[1])), 1e-3)
+        assert abs(np.linalg.norm(w) - 1) < tol and np.dot(w, nv) >= -tol
+        ind = -nv + 0.1 * r.standard_normal(3)
+        ind = (ind / np.linalg.norm(ind)).astype(np.float32)
+        L.orc_sample_phong((C.c_float * 3)(*nv), (C.c_float * 3)(*ind), 1000, (C.c_float * 2)(*u), out)
+        refl = ind - 2 * np.dot(ind, nv) * nv
+        assert np.dot(np.array(out), refl) > 0.9                                 # Ns=1000 lobe ~ mirror
+        L.orc_sample_fresnel((C.c_float * 3)(*nv), (C.c_float * 3)(*ind), 0.0, 1.5, (C.c_float * 1)(0.5), out)
+        assert np.allclose(np.array(out), refl, atol=1e-5)                       # Tr=0 -> mirror
+
+
+def test_transcendentals_close_to_libm(oracle_mod):
+    L = oracle_mod.lib()
+    x = np.linspace(0, 2 * np.pi, 5001).astype(np.float32)
+    s = np.array([L.orc_sinf(float(v)) for v in x], np.float32)
+    c = np.array([L.orc_cosf(float(v)) for v in x], np.float32)
+    rs = np.sin(x.astype(np.float64)).astype(np.float32)
+    rc = np.cos(x.astype(np.float64)).astype(np.float32)
+    ulp = lambda a, b: np.abs(a.view(np.int32).astype(np.int64) - b.view(np.int32).astype(np.int64))
+    assert np.max(ulp(s, rs)[np.abs(rs) > 1e-6]) <= 1 and np.max(ulp(c, rc)[np.abs(rc) > 1e-6]) <= 1
+    a = np.random.default_rng(4).random(3000).astype(np.float32)
+    for e in (5.0, 1 / 1001, 1 / 3):
+        p = np.array([L.orc_powf(float(v), e) for v in a], np.float32)
+        ref = np.power(a.astype(np.float64), np.float64(np.float32(e))).astype(np.float32)
+        assert np.max(ulp(p, ref)) <= 1
+
+
+def test_rng_is_minimal_standard_park_miller(oracle_mod):
+    import ctypes as C
+    L = oracle_mod.lib()
+    st = C.c_uint32(1)
+    seq = []
+    for _ in range(3):
+        L.orc_rng_next(C.byref(st))
+        seq.append(st.value)
+    assert seq == [16807, 282475249, 1622650073]
+    st = C.c_uint32(1)
+    for _ in range(10000):
+        L.orc_rng_next(C.byref(st))
+    assert st.value == 1043618065          # Park & Miller (1988) check value
+    keys = {L.orc_rng_init(p, 123, s) for p in range(64) for s in range(64)}
+    assert len(keys) == 64 * 64 and min(keys) >= 1 and max(keys) <= 0x7FFFFFFE
+
+
+def test_statistical_pin_against_reference_render(scenes, oracle_mod):
+    """CV/result1.png (1000 spp, 8-bit) was rendered with luminance 30 (MC.docx ¶58)
+    and without the Kd tint on Fresnel hits (the rtx.hlsl:345 form).  100x100
+    block means of an oracle render of that variant match it wherever the
+    reference is not saturated; the current-code variant (ILLUM 10, tinted
+    Fresnel) is clearly rejected by the same measure."""
+    from PIL import Image
+    ref = np.asarray(Image.open(os.path.join(GOLDEN, "result1.png")).convert("RGB")).astype(np.float32) / 255
+    blocks = lambda a: a.reshape(6, 100, 8, 100, 3).mean(axis=(1, 3))
+    unsat = ~(ref >= 254 / 255).reshape(6, 100, 8, 100, 3).any(axis=(1, 3, 4))
+    assert unsat.sum() >= 30
+    th = os.cpu_count() or 8
+    img, _ = scenes["scene01"].render(oracle_mod.RenderParams(width=800, height=600, spp=16, illum=30.0, fresnel_kd=0,
+                                                              traversal=oracle_mod.KD_ORDERED, threads=th))
+    d = np.abs(blocks(img) - blocks(ref))[unsat]
+    assert d.mean() < 0.004 and d.max() < 0.04, (d.mean(), d.max())
+    cur, _ = scenes["scene01"].render(oracle_mod.RenderParams(width=800, height=600, spp=16, illum=10.0, fresnel_kd=1,
+                                                              traversal=oracle_mod.KD_ORDERED, threads=th))
+    assert np.abs(blocks(cur) - blocks(ref))[unsat].mean() > 0.03
