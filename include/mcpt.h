@@ -112,6 +112,19 @@ int mcpt_device_count(int32_t* out);
 void mcpt_render_params_default(mcpt_render_params* p);
 
 /* ---- host model (ObjModel) ---------------------------------------------- */
+/* In-memory ObjModel, laid out like ObjReader.hpp:57-63 (element 0 of every
+ * array is the reference's dummy).  Groups in CSR form, any order (they are
+ * re-keyed by name like the reference's std::map).  Arrays are copied.     */
+typedef struct {
+    const float* vertices;        int64_t n_vertices;    /* 3 floats each  */
+    const float* normals;         int64_t n_normals;     /* 3 floats each  */
+    const int32_t* triangles;     int64_t n_triangles;   /* 10 ints each: v[3] t[3] n[3] material */
+    const double* materials;      int64_t n_materials;   /* 12 doubles each: Ka Kd Ks Ns Tr Ni */
+    const char* const* group_names;                      /* n_groups names */
+    const int64_t* group_offsets;                        /* n_groups+1 offsets into group_tris */
+    const int32_t* group_tris;    int64_t n_groups;
+} mcpt_model_desc;
+int mcpt_model_create(const mcpt_model_desc* d, mcpt_model** out);
 int mcpt_model_read_obj(const char* path, mcpt_model** out);
 void mcpt_model_free(mcpt_model* m);
 int mcpt_model_get_info(const mcpt_model* m, mcpt_model_info* out);

@@ -62,6 +62,17 @@ class RenderStats(C.Structure):
                 for n, _ in self._fields_ if n != "pad_"}
 
 
+class ModelDesc(C.Structure):
+    _fields_ = [
+        ("vertices", C.POINTER(C.c_float)), ("n_vertices", C.c_int64),
+        ("normals", C.POINTER(C.c_float)), ("n_normals", C.c_int64),
+        ("triangles", C.POINTER(C.c_int32)), ("n_triangles", C.c_int64),
+        ("materials", C.POINTER(C.c_double)), ("n_materials", C.c_int64),
+        ("group_names", C.POINTER(C.c_char_p)), ("group_offsets", C.POINTER(C.c_int64)),
+        ("group_tris", C.POINTER(C.c_int32)), ("n_groups", C.c_int64),
+    ]
+
+
 # every symbol include/mcpt.h declares, with its ctypes signature
 _vp = C.c_void_p
 _SIGS = {
@@ -70,6 +81,7 @@ _SIGS = {
     "mcpt_init": (C.c_int, [C.POINTER(C.c_int32), C.c_int32]),
     "mcpt_device_count": (C.c_int, [C.POINTER(C.c_int32)]),
     "mcpt_render_params_default": (None, [C.POINTER(RenderParamsC)]),
+    "mcpt_model_create": (C.c_int, [C.POINTER(ModelDesc), C.POINTER(_vp)]),
     "mcpt_model_read_obj": (C.c_int, [C.c_char_p, C.POINTER(_vp)]),
     "mcpt_model_free": (None, [_vp]),
     "mcpt_model_get_info": (C.c_int, [_vp, C.POINTER(ModelInfo)]),

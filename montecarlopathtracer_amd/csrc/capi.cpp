@@ -367,6 +367,56 @@ void mcpt_render_params_default(mcpt_render_params* p) {
     p->shard_count = 1;
 }
 
+int mcpt_model_create(const mcpt_model_desc* d, mcpt_model** out) {
+    return guarded([&]() -> int {
+        if (!d || !out) return fail(MCPT_E_INVALID, "NULL argument");
+        if (d->n_vertices < 1 || d->n_normals < 1 || d->n_triangles < 1 || d->n_materials < 1 || d->n_groups < 0)
+            return fail(MCPT_E_INVALID, "arrays must include the dummy element 0");
+        if (!d->vertices || !d->normals || !d->triangles || !d->materials ||
+            (d->n_groups > 0 && (!d->group_names || !d->group_offsets || !d->group_tris)))
+            return fail(MCPT_E_INVALID, "NULL array");
+        auto m = std::make_unique<mcpt_model>();
+        mcpt::ObjModel& o = m->m;
+        o.path = "<memory>";
+        o.vertices.resize(size_t(d->n_vertices));
+        for (int64_t i = 0; i < d->n_vertices; ++i)
+            o.vertices[size_t(i)] = mcpt::Vec3{d->vertices[3 * i], d->vertices[3 * i + 1], d->vertices[3 * i + 2]};
+        o.normals.resize(size_t(d->n_normals));
+        for (int64_t i = 0; i < d->n_normals; ++i)
+            o.normals[size_t(i)] = mcpt::Vec3{d->normals[3 * i], d->normals[3 * i + 1], d->normals[3 * i + 2]};
+        o.n_texcoords = 1;
+        o.triangles.resize(size_t(d->n_triangles));
+        for (int64_t i = 0; i < d->n_triangles; ++i) {
+            const int32_t* t = d->triangles + 10 * i;
+            auto& dst = o.triangles[size_t(i)];
+            for (int j = 0; j < 3; ++j) { dst.v[j] = t[j]; dst.t[j] = t[3 + j]; dst.n[j] = t[6 + j]; }
+            dst.material = t[9];
+            if (i > 0 && (t[9] < 0 || t[9] >= d->n_materials)) return fail(MCPT_E_INVALID, "material index out of range");
+        }
+        o.materials.resize(size_t(d->n_materials));
+        for (int64_t i = 0; i < d->n_materials; ++i) {
+            const double* q = d->materials + 12 * i;
+            auto& mt = o.materials[size_t(i)];
+            mt.Ka = mcpt::Vec3{float(q[0]), float(q[1]), float(q[2])};
+            mt.Kd = mcpt::Vec3{float(q[3]), float(q[4]), float(q[5])};
+            mt.Ks = mcpt::Vec3{float(q[6]), float(q[7]), float(q[8])};
+            mt.Ns = q[9]; mt.Tr = q[10]; mt.Ni = q[11];
+        }
+        for (int64_t g = 0; g < d->n_groups; ++g) {
+            const int64_t b = d->group_offsets[g], e = d->group_offsets[g + 1];
+            if (b < 0 || e < b) return fail(MCPT_E_INVALID, "bad group offsets");
+            auto& dst = o.groups[d->group_names[g] ? d->group_names[g] : ""];
+            for (int64_t k = b; k < e; ++k) {
+                if (d->group_tris[k] < 1 || d->group_tris[k] >= d->n_triangles)
+                    return fail(MCPT_E_INVALID, "group triangle index out of range");
+                dst.push_back(d->group_tris[k]);
+            }
+        }
+        *out = m.release();
+        return MCPT_OK;
+    });
+}
+
 int mcpt_model_read_obj(const char* path, mcpt_model** out) {
     return guarded([&]() -> int {
         if (!path || !out) return fail(MCPT_E_INVALID, "path/out is NULL");

@@ -59,6 +59,36 @@ class ObjModel:
 
     readObj = read_obj
 
+    @classmethod
+    def from_arrays(cls, vertices, normals, triangles, materials, groups: dict) -> "ObjModel":
+        """Build from in-memory arrays laid out like ObjReader.hpp:57-63 (element 0 = dummy):
+        vertices (n,3), normals (n,3), triangles (n,10) v/t/n/material, materials (n,12)
+        Ka Kd Ks Ns Tr Ni, groups {name: triangle indices}."""
+        v = np.ascontiguousarray(vertices, np.float32)
+        n = np.ascontiguousarray(normals, np.float32)
+        t = np.ascontiguousarray(triangles, np.int32)
+        m = np.ascontiguousarray(materials, np.float64)
+        names = list(groups)
+        offs = np.zeros(len(names) + 1, np.int64)
+        for i, k in enumerate(names):
+            offs[i + 1] = offs[i] + len(groups[k])
+        gt = np.ascontiguousarray(np.concatenate([np.asarray(groups[k], np.int32) for k in names])
+                                  if names else np.zeros(0, np.int32), np.int32)
+        cnames = (C.c_char_p * max(len(names), 1))(*[k.encode() for k in names])
+        d = _capi.ModelDesc()
+        d.vertices, d.n_vertices = v.ctypes.data_as(C.POINTER(C.c_float)), v.shape[0]
+        d.normals, d.n_normals = n.ctypes.data_as(C.POINTER(C.c_float)), n.shape[0]
+        d.triangles, d.n_triangles = t.ctypes.data_as(C.POINTER(C.c_int32)), t.shape[0]
+        d.materials, d.n_materials = m.ctypes.data_as(C.POINTER(C.c_double)), m.shape[0]
+        d.group_names, d.group_offsets = cnames, offs.ctypes.data_as(C.POINTER(C.c_int64))
+        d.group_tris, d.n_groups = gt.ctypes.data_as(C.POINTER(C.c_int32)), len(names)
+        h = C.c_void_p()
+        check(lib().mcpt_model_create(C.byref(d), C.byref(h)))
+        obj = cls()
+        obj._h = h
+        obj.path = "<memory>"
+        return obj
+
     def _free(self):
         if self._h is not None and _capi._lib is not None:
             _capi._lib.mcpt_model_free(self._h)

@@ -66,3 +66,12 @@ def test_shards_partition_the_image(mcpt, W, H, T, N):
             first = xy[ok][0]
             assert first[0] % T == 0 and first[1] % T == 0
     assert total == W * H and (seen == 1).all()
+
+
+def test_pw_tracer_adapter_compiles_and_links(mcpt):
+    """include/mcpt_pw_tracer.hpp: reference-style PW::Tracer calls compile and link
+    against libmcpt.so (run on the GPU in tests/test_gpu_parity.py)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests", "cpp"))
+    import build_dropin
+    assert os.path.exists(build_dropin.build())

@@ -1,0 +1,74 @@
+"""GPU path at BASELINE sizes, through size-independent properties, plus the
+statistical pin against the reference's own 1000-spp render.
+
+* 1024x1024 @ 1024 spp (BASELINE configs[1]): rendering the 8 interleaved
+  tile shards (configs[2]'s partition) and reassembling them reproduces the
+  single-GPU image bit for bit; a second render is bit-identical (determinism);
+  the image is finite and the light is the brightest region.
+* RenderScene's progressive loop (10 launches x 100 spp, prevCount running
+  mean, CUTracer.cu:378-398) at 800x600 with the published-render variant
+  (luminance 30, untinted Fresnel) matches CV/result1.png statistically.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module")
+def scene01(mcpt):
+    return mcpt.Scene(mcpt.ObjModel(mcpt.scene_path("scene01")))
+
+
+def test_fullsize_shards_and_determinism(mcpt, scene01):
+    import torch
+    W = H = 1024
+    p = mcpt.RenderParams(width=W, height=H, spp=1024, spp_chunk=32)
+    full = torch.zeros((H * W, 4), dtype=torch.float32, device="cuda")
+    scene01.render_device(p, full.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    again = torch.zeros_like(full)
+    scene01.render_device(p, again.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    st = scene01.stats()
+    assert st["renders"] == 2 and st["rays"] > 2 * 3.0e9
+    assert torch.equal(full, again)
+    img = full.view(H, W, 4)[..., :3].cpu().numpy()
+    assert np.isfinite(img).all() and img.min() >= 0
+    b = img.mean(axis=2).reshape(32, 32, 32, 32).mean(axis=(1, 3))     # 32x32-pixel blocks
+    by, bx = np.unravel_index(np.argmax(b), b.shape)
+    assert b.max() > 5 * img.mean() and by < 12 and 10 <= bx <= 21      # ceiling light, centred, upper part
+    N = 8
+    got = torch.full((H * W, 4), -1.0, dtype=torch.float32, device="cuda")
+    for r in range(N):
+        ps = mcpt.RenderParams(width=W, height=H, spp=1024, spp_chunk=32, shard_count=N, shard_index=r)
+        part = torch.zeros((ps.output_pixels(), 4), dtype=torch.float32, device="cuda")
+        scene01.render_device(ps, part.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        xy = torch.from_numpy(ps.shard_pixels().astype(np.int64)).cuda()
+        ok = xy[:, 0] >= 0
+        got[(xy[:, 1] * W + xy[:, 0])[ok]] = part[ok]
+    torch.cuda.synchronize()
+    scene01.stats()
+    assert torch.equal(got[:, :3], full[:, :3])
+
+
+def test_progressive_render_matches_reference_image(mcpt):
+    from PIL import Image
+    ref = np.asarray(Image.open(os.path.join(GOLDEN, "result1.png")).convert("RGB")).astype(np.float32) / 255
+    tr = mcpt.Tracer()
+    tr.initialize([0])
+    tr.create_geometry(mcpt.ObjModel(mcpt.scene_path("scene01")))
+    host = np.zeros((600, 800, 3), np.float32)
+    tr.render_scene(1, host, num_kernels=10, samples_per_kernel=100, illum=30.0, fresnel_kd=False)
+    tr.destroy_geometry()
+    enc = mcpt.encode_8bit(host).astype(np.float32) / 255
+    blocks = lambda a: a.reshape(6, 100, 8, 100, 3).mean(axis=(1, 3))
+    unsat = ~(ref >= 254 / 255).reshape(6, 100, 8, 100, 3).any(axis=(1, 3, 4))
+    d = np.abs(blocks(host) - blocks(ref))[unsat]
+    assert d.mean() < 0.003 and d.max() < 0.03, (d.mean(), d.max())
+    rmse = float(np.sqrt(np.mean((enc - ref) ** 2)))
+    # per-pixel: both images carry 1000-spp Monte Carlo noise (the reference's own
+    # 100-vs-1000 spp RMSE is 0.031); the block means above carry the bias test
+    assert rmse < 0.05, rmse

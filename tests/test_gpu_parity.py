@@ -95,3 +95,23 @@ def test_device_render_deterministic(mcpt):
     assert np.array_equal(outs[0], outs[1])
     host, _ = scene.render(p)
     assert np.array_equal(outs[0][..., :3], host)
+
+
+def test_pw_tracer_adapter_matches_abi(mcpt, tmp_path):
+    """Reference-style call sequence through include/mcpt_pw_tracer.hpp renders what
+    the Python mirror renders (RenderScene: 3 launches x 4 spp, prevCount mean)."""
+    import os
+    import subprocess
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "cpp"))
+    import build_dropin
+    exe = build_dropin.build()
+    out = str(tmp_path / "img.bin")
+    r = subprocess.run([exe, mcpt.scene_path("scene01"), out], capture_output=True, text=True)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+    got = np.fromfile(out, np.float32).reshape(30, 40, 3)
+    tr = mcpt.Tracer()
+    tr.create_geometry(mcpt.ObjModel(mcpt.scene_path("scene01")))
+    host = np.zeros((30, 40, 3), np.float32)
+    tr.render_scene(1, host, num_kernels=3, samples_per_kernel=4)
+    assert np.array_equal(got, host)

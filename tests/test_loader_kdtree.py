@@ -174,3 +174,27 @@ def test_kd_build_synthetic_matches_oracle(mcpt, oracle_mod, tmp_path, kind):
     path = _write(tmp_path, _soup_obj(tris.astype(np.float32)), "")
     s = _assert_same(mcpt, oracle_mod, path)
     assert s.info()["n_triangles"] == len(tris)
+
+
+@pytest.mark.parametrize("name", ["scene01", "scene03"])
+def test_in_memory_model_equals_file_model(mcpt, name):
+    """mcpt_model_create (CreateGeometry's in-memory ObjModel input) == the file reader."""
+    m = mcpt.ObjModel(mcpt.scene_path(name))
+    groups = m.groups()
+    rev = dict(reversed(list(groups.items())))          # order must not matter (std::map)
+    m2 = mcpt.ObjModel.from_arrays(m.vertices(), m.normals(), m.triangles(), m.materials(), rev)
+    assert list(m2.groups()) == list(groups)
+    a = mcpt.Scene(m, host_only=True).kd()
+    b = mcpt.Scene(m2, host_only=True).kd()
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+
+
+def test_in_memory_model_rejects_bad_indices(mcpt):
+    v = np.zeros((4, 3), np.float32); n = np.zeros((2, 3), np.float32)
+    t = np.zeros((2, 10), np.int32); t[1, :3] = [1, 2, 3]; t[1, 6:9] = 1
+    mats = np.zeros((1, 12)); mats[0, 9] = 1; mats[0, 11] = 1
+    with pytest.raises(mcpt.McptError):
+        mcpt.ObjModel.from_arrays(v, n, t, mats, {"g": [5]})
+    m = mcpt.ObjModel.from_arrays(v, n, t, mats, {"g": [1]})
+    assert m.info()["n_triangles"] == 2
