@@ -15,13 +15,13 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "lib")
-LIB = os.path.join(LIBDIR, "libmcpt.so")
+LIB = os.path.join(LIBDIR, os.environ.get("MCPT_LIB_NAME", "libmcpt.so"))
 SOURCES = ["host_model.cpp", "capi.cpp", "render.hip"]
 HEADERS = ["host_model.hpp", "mcpt_device.hpp", "render_launch.hpp"]
 ARCH = os.environ.get("MCPT_OFFLOAD_ARCH", "gfx950")
 
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-Wall",
-          "-I" + os.path.join(ROOT, "include")]
+          "-I" + os.path.join(ROOT, "include")] + os.environ.get("MCPT_EXTRA_FLAGS", "").split()
 
 
 def _hipcc() -> str:
@@ -46,7 +46,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     hipcc = _hipcc()
 
     def compile_one(src):
-        obj = os.path.join(LIBDIR, "obj", src + ".o")
+        obj = os.path.join(LIBDIR, "obj", os.path.basename(LIB) + "." + src + ".o")
         lang = (["-x", "hip", f"--offload-arch={ARCH}"] if src.endswith(".hip")
                 else ["-x", "c++", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include"])
         cmd = [hipcc] + lang + COMMON + ["-c", os.path.join(CSRC, src), "-o", obj]

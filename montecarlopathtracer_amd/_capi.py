@@ -18,7 +18,7 @@ except Exception:  # pragma: no cover - torch is optional for host-only use
     torch = None
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libmcpt.so")
+LIB_PATH = os.environ.get("MCPT_LIB_PATH") or os.path.join(_HERE, "lib", "libmcpt.so")
 
 MCPT_OK = 0
 ERRORS = {-1: "INVALID", -2: "IO", -3: "PARSE", -4: "DEVICE", -5: "NOMEM", -6: "UNSUPPORTED"}

@@ -129,7 +129,9 @@ void build_image(mcpt_scene& s) {
     auto al16 = [](size_t x) { return (x + 15u) & ~size_t(15); };
     const size_t off_tris = 0;
     const size_t off_nodes = al16(off_tris + size_t(nt) * 48);
-    const size_t off_leafs = al16(off_nodes + size_t(nn) * 8);
+    // nodes are stored one slot late (slot 0 = padding): BFS puts every sibling
+    // pair at odd indices [2k+1, 2k+2], so each pair becomes one aligned 16-B record
+    const size_t off_leafs = al16(off_nodes + size_t(nn + 1) * 8);
     const size_t off_geoms = al16(off_leafs + size_t(nl) * 4);
     const size_t total = al16(off_geoms + size_t(ng) * 64);
     if (total > 0xFFFFFFF0u) throw mcpt::Error{MCPT_E_UNSUPPORTED, "scene image exceeds 4 GiB"};
@@ -155,7 +157,9 @@ void build_image(mcpt_scene& s) {
             w[0] = (3u << 30) | n.leaf_begin;
             w[1] = n.leaf_count;
         }
-        std::memcpy(img + off_nodes + size_t(i) * 8, w, 8);
+        if (n.axis && (n.left % 2u) != 1u) throw mcpt::Error{MCPT_E_INVALID, "KD sibling pair not at an odd index"};
+        std::memcpy(img + off_nodes + size_t(i + 1) * 8, w, 8);
+        if (i == 0) { s.gpu.root_w[0] = w[0]; s.gpu.root_w[1] = w[1]; }
     }
     if (nl) std::memcpy(img + off_leafs, hs.leaf_ids.data(), size_t(nl) * 4);
     for (uint32_t g = 0; g < ng; ++g) {
@@ -251,8 +255,8 @@ Plan make_plan(const mcpt_scene& s, const mcpt_render_params* p) {
 void prepare_workspace(mcpt_scene& s, mcpt::KernelParams& k) {
     ensure_buf(s.ws.partial, s.ws.partial_bytes, size_t(k.nchunks) * k.npix_local * 16);
     if (!s.ws.small) {
-        HIP_TRY(hipMalloc(&s.ws.small, 128));
-        HIP_TRY(hipMemset(s.ws.small, 0, 128));
+        HIP_TRY(hipMalloc(&s.ws.small, 256));
+        HIP_TRY(hipMemset(s.ws.small, 0, 256));
     }
     const size_t lanes = static_cast<size_t>(mcpt::total_lanes_for(s.gpu.image_bytes, s.cus));
     ensure_buf(s.ws.spill, s.ws.spill_bytes, 32 * lanes * 16);
@@ -305,9 +309,12 @@ void read_stats(mcpt_scene& s, mcpt_render_stats* out) {
     }
     s.pending.clear();
     if (s.ws.small) {
-        unsigned long long st[8];
+        unsigned long long st[16];
         HIP_TRY(hipMemcpy(st, static_cast<char*>(s.ws.small) + 64, sizeof st, hipMemcpyDeviceToHost));
-        HIP_TRY(hipMemset(static_cast<char*>(s.ws.small) + 64, 0, 64));
+        HIP_TRY(hipMemset(static_cast<char*>(s.ws.small) + 64, 0, sizeof st));
+        if (st[8] | st[9] | st[10] | st[11])   // diagnostic builds (-DMCPT_PHASE_TIMING) only
+            std::fprintf(stderr, "mcpt phase cycles (sum over waves): units %llu trav %llu shade %llu burst_iters %llu\n",
+                         st[8], st[9], st[10], st[11]);
         r.rays = st[0]; r.paths = st[1]; r.inner_visits = st[2]; r.leaf_visits = st[3];
         r.leaf_refs = st[4]; r.tri_tests = st[5]; r.shades = st[6]; r.stack_spills = st[7];
     }

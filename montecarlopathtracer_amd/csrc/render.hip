@@ -52,7 +52,7 @@ struct RayState {
     V3 o, d;
     float ix, iy, iz;
     float tmin, tmax, best;
-    uint32_t node, bprio;
+    uint32_t nw0, nw1, bprio;            // current node record
     int32_t sp, htri;
     float hbeta, hgamma;
 };
@@ -66,7 +66,8 @@ __device__ __forceinline__ bool begin_ray(RayState& r, const GpuScene& sc) {
     r.hbeta = r.hgamma = 0.0f;
     r.best = kFltMax;
     r.bprio = 0xFFFFFFFFu;
-    r.node = 0;
+    r.nw0 = sc.root_w[0];
+    r.nw1 = sc.root_w[1];
     r.sp = 0;
     float tmin = 0.0f, tmax = kFltMax;
     const float oo[3] = {r.o.x, r.o.y, r.o.z}, dd[3] = {r.d.x, r.d.y, r.d.z}, inv[3] = {r.ix, r.iy, r.iz};
@@ -123,51 +124,53 @@ __device__ __forceinline__ void test_tri(RayState& r, const float4* __restrict__
 }
 
 // One resumable traversal iteration: descend to a leaf, test it, pop.
-// Returns true when the ray's closest hit is final.
+// Returns true when the ray's closest hit is final.  The children of the
+// current node are read as one 16-B sibling-pair record whose address is known
+// before the split-plane decision, so the LDS latency overlaps the decision;
+// stack entries carry the far child's record (16 B: w0, w1, lo, hi), so a pop
+// needs no node re-read.
 template <int S>
 __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict__ tris,
-                                          const uint2* __restrict__ nodes, const uint32_t* __restrict__ leafs,
-                                          uint32_t* st_node, float* st_lo, float* st_hi, int stride,
-                                          uint4* __restrict__ spill, uint32_t spill_stride, Counters& c) {
-    uint2 nd = nodes[r.node];
-    while ((nd.x >> 30) != 3u) {
+                                          const uint2* __restrict__ nodes1, const uint32_t* __restrict__ leafs,
+                                          uint4* st, int stride, uint4* __restrict__ spill, uint32_t spill_stride,
+                                          Counters& c) {
+    uint32_t w0 = r.nw0, w1 = r.nw1;
+    while ((w0 >> 30) != 3u) {
         c.inner++;
-        const int a = (int)(nd.x >> 30);
-        const float sv = __uint_as_float(nd.y);
-        const uint32_t left = nd.x & 0x3FFFFFFFu;
+        const uint32_t left = w0 & 0x3FFFFFFFu;
+        const uint4 pr = *reinterpret_cast<const uint4*>(nodes1 + left);   // children left, left+1
+        const int a = (int)(w0 >> 30);
+        const float sv = __uint_as_float(w1);
         const float oa = sel3(a, r.o.x, r.o.y, r.o.z);
         const float da = sel3(a, r.d.x, r.d.y, r.d.z);
         const float ia = sel3(a, r.ix, r.iy, r.iz);
         const float t = (sv - oa) * ia;
         const bool below = (oa < sv) || (oa == sv && da <= 0.0f);
-        const uint32_t nearc = below ? left : left + 1;
-        const uint32_t farc = below ? left + 1 : left;
         // if/else chain of the oracle, evaluated branch-free
         const bool pp = (da == 0.0f) & (oa == sv);                  // ray inside the plane: both
         const bool no = !(t > 0.0f) | (t > r.tmax * kEpsHi);        // near child only
         const bool fo = t * kEpsHi < r.tmin;                        // far child only
         const bool go_far = !pp & !no & fo;
         const bool push_it = pp | (!no & !fo);
+        const uint32_t n0 = below ? pr.x : pr.z, n1 = below ? pr.y : pr.w;     // near child record
+        const uint32_t f0 = below ? pr.z : pr.x, f1 = below ? pr.w : pr.y;     // far child record
         if (push_it) {
             const float plo = pp ? r.tmin : (t > r.tmin ? t : r.tmin);
-            const int slot = (r.sp & (S - 1)) * stride;
+            uint4* slot = st + (r.sp & (S - 1)) * stride;
             if (r.sp >= S) {
-                spill[(uint32_t)(r.sp - S) * spill_stride] = make_uint4(st_node[slot], __float_as_uint(st_lo[slot]),
-                                                                        __float_as_uint(st_hi[slot]), 0u);
+                spill[(uint32_t)(r.sp - S) * spill_stride] = *slot;
                 c.spills++;
             }
-            st_node[slot] = farc;
-            st_lo[slot] = plo;
-            st_hi[slot] = r.tmax;
+            *slot = make_uint4(f0, f1, __float_as_uint(plo), __float_as_uint(r.tmax));
             r.sp++;
             if (!pp) r.tmax = t < r.tmax ? t : r.tmax;
         }
-        r.node = go_far ? farc : nearc;
-        nd = nodes[r.node];
+        w0 = go_far ? f0 : n0;
+        w1 = go_far ? f1 : n1;
     }
     c.leaf++;
-    const uint32_t begin = nd.x & 0x3FFFFFFFu;
-    const uint32_t cnt = nd.y;
+    const uint32_t begin = w0 & 0x3FFFFFFFu;
+    const uint32_t cnt = w1;
     for (uint32_t i = 0; i < cnt; i++) {
         c.refs++;
         c.tests++;
@@ -175,16 +178,13 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
     }
     if (r.sp == 0) return true;
     r.sp--;
-    const int slot = (r.sp & (S - 1)) * stride;
-    r.node = st_node[slot];
-    r.tmin = st_lo[slot];
-    r.tmax = st_hi[slot];
-    if (r.sp >= S) {
-        const uint4 e = spill[(uint32_t)(r.sp - S) * spill_stride];
-        st_node[slot] = e.x;
-        st_lo[slot] = __uint_as_float(e.y);
-        st_hi[slot] = __uint_as_float(e.z);
-    }
+    uint4* slot = st + (r.sp & (S - 1)) * stride;
+    const uint4 e = *slot;
+    r.nw0 = e.x;
+    r.nw1 = e.y;
+    r.tmin = __uint_as_float(e.z);
+    r.tmax = __uint_as_float(e.w);
+    if (r.sp >= S) *slot = spill[(uint32_t)(r.sp - S) * spill_stride];
     return r.best <= r.tmin * kEpsLo;
 }
 
@@ -237,19 +237,16 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
         for (uint32_t i = (uint32_t)tid; i < n16; i += BLOCK) dst[i] = src[i];
         __syncthreads();
         tris = reinterpret_cast<const float4*>(smem + sc.off_tris);
-        nodes = reinterpret_cast<const uint2*>(smem + sc.off_nodes);
+        nodes = reinterpret_cast<const uint2*>(smem + sc.off_nodes) + 1;   // node i at slot i+1
         leafs = reinterpret_cast<const uint32_t*>(smem + sc.off_leafs);
         geoms = reinterpret_cast<const GpuGeom*>(smem + sc.off_geoms);
     } else {
         tris = reinterpret_cast<const float4*>(sc.image + sc.off_tris);
-        nodes = reinterpret_cast<const uint2*>(sc.image + sc.off_nodes);
+        nodes = reinterpret_cast<const uint2*>(sc.image + sc.off_nodes) + 1;
         leafs = reinterpret_cast<const uint32_t*>(sc.image + sc.off_leafs);
         geoms = reinterpret_cast<const GpuGeom*>(sc.image + sc.off_geoms);
     }
-    unsigned char* stk = smem + kp.lds_stack_off;
-    uint32_t* st_node = reinterpret_cast<uint32_t*>(stk) + tid;
-    float* st_lo = reinterpret_cast<float*>(stk + (size_t)S * BLOCK * 4) + tid;
-    float* st_hi = reinterpret_cast<float*>(stk + (size_t)2 * S * BLOCK * 4) + tid;
+    uint4* st = reinterpret_cast<uint4*>(smem + kp.lds_stack_off) + tid;   // [S][BLOCK] x 16 B
     const uint32_t gl = blockIdx.x * BLOCK + (uint32_t)tid;
     uint4* spill = kp.spill + gl;
     const uint32_t spill_stride = kp.total_lanes;
@@ -279,6 +276,13 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
         mode = begin_ray(r, sc) ? kTrav : kReady;
     };
 
+#ifdef MCPT_PHASE_TIMING
+    unsigned long long tm_units = 0, tm_trav = 0, tm_shade = 0, tm_iters = 0, tm_t0;
+#define MCPT_STAMP(acc) do { unsigned long long t1_ = __builtin_amdgcn_s_memtime(); acc += t1_ - tm_t0; tm_t0 = t1_; } while (0)
+    tm_t0 = __builtin_amdgcn_s_memtime();
+#else
+#define MCPT_STAMP(acc) do {} while (0)
+#endif
     for (;;) {
         // ---- work units: one atomic per wave for every lane that needs one ----
         for (;;) {
@@ -309,17 +313,22 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
             }
         }
         if (!__ballot(mode != kDead)) break;
+        MCPT_STAMP(tm_units);
 
         // ---- traversal burst: until half the wave is ready to shade --------
         for (;;) {
+#ifdef MCPT_PHASE_TIMING
+            tm_iters++;
+#endif
             if (mode == kTrav) {
-                if (trav_iter<S>(r, tris, nodes, leafs, st_node, st_lo, st_hi, BLOCK, spill, spill_stride, c))
+                if (trav_iter<S>(r, tris, nodes, leafs, st, BLOCK, spill, spill_stride, c))
                     mode = kReady;
             }
             const uint64_t trv = __ballot(mode == kTrav);
             const uint64_t rdy = __ballot(mode == kReady);
             if (!trv || __popcll(rdy) >= kp.ready_thresh) break;
         }
+        MCPT_STAMP(tm_trav);
 
         // ---- shading round for every ready lane (CUTracer.cu:105-175) -------
         if (mode == kReady) {
@@ -367,7 +376,7 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
                         depth++;
                         c.rays++;
                         mode = begin_ray(r, sc) ? kTrav : kReady;
-                    }
+                                    }
                 }
             } else {
                 if (r.htri >= 0) {
@@ -396,8 +405,17 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
                 }
             }
         }
+        MCPT_STAMP(tm_shade);
     }
 
+#ifdef MCPT_PHASE_TIMING
+    if (lane == 0) {
+        atomicAdd(kp.stats + 8, tm_units);
+        atomicAdd(kp.stats + 9, tm_trav);
+        atomicAdd(kp.stats + 10, tm_shade);
+        atomicAdd(kp.stats + 11, tm_iters);
+    }
+#endif
     // ---- counters: wave reduction, one atomic per wave per counter --------
     uint32_t vals[8] = {c.rays, c.paths, c.inner, c.leaf, c.refs, c.tests, c.shades, c.spills};
 #pragma unroll
@@ -450,7 +468,7 @@ hipError_t launch_path(const KernelParams& kp, int grid, size_t lds, hipStream_t
 }  // namespace
 
 // LDS need of the in-LDS variant for a scene image of `image_bytes`
-size_t lds_bytes_in_lds(uint32_t image_bytes, int S) { return (size_t)image_bytes + (size_t)S * kLdsBlock * 12; }
+size_t lds_bytes_in_lds(uint32_t image_bytes, int S) { return (size_t)image_bytes + (size_t)S * kLdsBlock * 16; }
 
 hipError_t launch_render(const KernelParams& kp_in, int cus, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1,
                          hipEvent_t ev2, float4* fb, int* variant_out) {
@@ -470,7 +488,7 @@ hipError_t launch_render(const KernelParams& kp_in, int cus, hipStream_t st, hip
         e = launch_path<true, 4, kLdsBlock>(kp, cus, lds_bytes_in_lds(img, 4), st);
     } else {
         variant = 3;
-        e = launch_path<false, 8, kGlobalBlock>(kp, cus * kGlobalBlocksPerCu, (size_t)8 * kGlobalBlock * 12, st);
+        e = launch_path<false, 8, kGlobalBlock>(kp, cus * kGlobalBlocksPerCu, (size_t)8 * kGlobalBlock * 16, st);
     }
     if (e != hipSuccess) return e;
     if (ev1) hipEventRecord(ev1, st);

@@ -4,8 +4,10 @@
 // same bytes are copied verbatim into LDS by the in-LDS kernel variant):
 //   tris   3 x float4 per KD triangle: (a.xyz, brute-force rank bits),
 //          (a-b .xyz, geometry index bits), (a-c .xyz, 0)       48 B
-//   nodes  uint2 per KD node (BFS): inner  x = axis<<30 | left child,
-//          y = split value bits; leaf x = 3<<30 | first leaf ref, y = count  8 B
+//   nodes  uint2 per KD node (BFS), stored one slot late so that every
+//          sibling pair (left, left+1; left is odd in BFS order) is one aligned
+//          16-B record: inner x = axis<<30 | left child, y = split value bits;
+//          leaf x = 3<<30 | first leaf ref, y = count                       8 B
 //   leafs  uint32 KD triangle id per leaf reference                    4 B
 //   geoms  GpuGeom per geometry (material of CUTracer.cu:300-308)      64 B
 // Shading normals live outside the image (read once per shaded hit):
@@ -37,6 +39,7 @@ struct GpuScene {
     uint32_t off_tris, off_nodes, off_leafs, off_geoms;
     uint32_t n_tris, n_nodes, n_leafs, n_geoms;
     float root_min[3], root_max[3];
+    uint32_t root_w[2];                  // root node record (nodes[0])
 };
 
 struct KernelParams {
