@@ -20,7 +20,7 @@ SOURCES = ["host_model.cpp", "capi.cpp", "render.hip"]
 HEADERS = ["host_model.hpp", "mcpt_device.hpp", "render_launch.hpp"]
 ARCH = os.environ.get("MCPT_OFFLOAD_ARCH", "gfx950")
 
-COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-Wall",
+COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-fno-slp-vectorize", "-Wall",
           "-I" + os.path.join(ROOT, "include")] + os.environ.get("MCPT_EXTRA_FLAGS", "").split()
 
 

@@ -101,12 +101,15 @@ __device__ __forceinline__ void test_tri(RayState& r, const float4* __restrict__
     const float qb = det3(aox, A2.x, r.d.x, aoy, A2.y, r.d.y, aoz, A2.z, r.d.z);
     const float qg = det3(A1.x, aox, r.d.x, A1.y, aoy, r.d.y, A1.z, aoz, r.d.z);
     const float qt = det3(A1.x, A2.x, aox, A1.y, A2.y, aoy, A1.z, A2.z, aoz);
+    // sign-normalised numerators: beta, gamma, t > 0 needs all three > 0 (a NaN
+    // anywhere means no hit, so min3 may drop it); detA == 0 fails the magnitude test
     const uint32_t sA = __float_as_uint(detA) & 0x80000000u;
-    const bool signs_ok = ((__float_as_uint(qb) & 0x80000000u) == sA) & ((__float_as_uint(qg) & 0x80000000u) == sA) &
-                          ((__float_as_uint(qt) & 0x80000000u) == sA) & (qb != 0.0f) & (qg != 0.0f) &
-                          (qt != 0.0f) & (detA != 0.0f);
+    const float xb = __uint_as_float(__float_as_uint(qb) ^ sA);
+    const float xg = __uint_as_float(__float_as_uint(qg) ^ sA);
+    const float xt = __uint_as_float(__float_as_uint(qt) ^ sA);
+    const bool signs_ok = __builtin_fminf(__builtin_fminf(xb, xg), xt) > 0.0f;
     const float adet = fabsf(detA) * 1.00000095367431640625f;   // 1 + 2^-20
-    const bool mags_ok = !(fabsf(qb) + fabsf(qg) > adet) & !(fabsf(qt) > r.best * adet);
+    const bool mags_ok = !(xb + xg > adet) & !(xt > r.best * adet);
     if (signs_ok & mags_ok) {
         const float beta = qb / detA;
         const float gamma = qg / detA;

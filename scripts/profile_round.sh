@@ -1,8 +1,9 @@
 #!/bin/bash
 # Collect the committed profile set for one round (run on the GPU box via gpurun).
 #   $1 = tag (e.g. r01)
-# kernel trace + stats, then separate PMC passes (FETCH_SIZE / WRITE_SIZE / SQ),
-# per MI355X_MICROARCH.md "rocprofv3 PMC slots".
+# kernel trace + stats, then separate PMC passes (FETCH_SIZE / WRITE_SIZE / SQ
+# groups / GRBM), per MI355X_MICROARCH.md "rocprofv3 PMC slots"; then
+# scripts/pmc_summary.py folds them into pmc_summary.json.
 set -e
 TAG=${1:-r01}
 R=$PWD
@@ -11,8 +12,18 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 cd /tmp
 B="python3 $R/bench.py --no-cpu-baseline"
+timeout -k 10 300 python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/bench.jsonl 2> $OUT/bench.err
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o run -- $B --steps 2 --warmup 1 > $OUT/kt.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- $B --steps 1 --warmup 0 > $OUT/fetch.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- $B --steps 1 --warmup 0 > $OUT/write.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VMEM --output-format csv -d $OUT/sq -o run -- $B --steps 1 --warmup 0 > $OUT/sq.log 2>&1
+pass() {   # name counters...
+  local n=$1; shift
+  timeout -k 10 300 rocprofv3 --pmc "$@" --output-format csv -d $OUT/$n -o run -- $B --steps 1 --warmup 0 > $OUT/$n.log 2>&1
+}
+pass fetch FETCH_SIZE
+pass write WRITE_SIZE
+pass sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VMEM
+pass sq_stall SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_WAIT_INST_LDS
+pass sq_lanes SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_FLOPS_FP32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT32 SQ_INSTS_BRANCH SQ_INSTS_VALU_CVT
+pass grbm GRBM_GUI_ACTIVE GRBM_COUNT
+cd $R
+python3 scripts/pmc_summary.py $OUT > $OUT/pmc_summary.json
 echo done
