@@ -93,7 +93,7 @@ def main():
     M.Tracer().initialize([dev.index])
 
     scene = M.Scene(M.ObjModel(M.scene_path(args.scene)))
-    scene_id = 1 if args.scene == "scene01" else 2
+    scene_id = 2 if args.scene in ("scene02", "scene03") else 1
     p = M.RenderParams.for_scene(scene_id, width=args.width, height=args.height, spp=args.spp,
                                  spp_chunk=args.spp_chunk, tile=8, shard_count=world, shard_index=rank,
                                  packed=world > 1)

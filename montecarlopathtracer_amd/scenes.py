@@ -15,6 +15,7 @@ import tempfile
 _HERE = os.path.dirname(os.path.abspath(__file__))
 SCENE_DIR = os.path.join(_HERE, "scenes")
 BUNDLED = ("scene01", "scene02", "scene03")
+GENERATED = ("cornell_bunny70k",)   # meshgen.cornell_mesh_scene (C4 workload)
 
 
 def _cache_dir() -> str:
@@ -25,10 +26,13 @@ def _cache_dir() -> str:
 
 def scene_path(name: str) -> str:
     """Return a filesystem path to ``<name>.obj`` (with its .mtl beside it)."""
+    if name in GENERATED:
+        from .meshgen import cornell_mesh_scene
+        return cornell_mesh_scene(name)
     if name not in BUNDLED:
         if os.path.exists(name):
             return name
-        raise FileNotFoundError(f"unknown scene {name!r}; bundled: {BUNDLED}")
+        raise FileNotFoundError(f"unknown scene {name!r}; bundled: {BUNDLED}, generated: {GENERATED}")
     out = _cache_dir()
     for ext in ("obj", "mtl"):
         dst = os.path.join(out, f"{name}.{ext}")

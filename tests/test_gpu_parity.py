@@ -20,6 +20,7 @@ CASES = [
     ("scene01", 40, 24, 4, 3, 12, 99, 1, 10.0),
     ("scene02", 48, 36, 4, 2, 7, 5, 1, 10.0),
     ("scene03", 40, 30, 4, 4, 7, 11, 1, 10.0),
+    ("cornell_bunny70k", 48, 40, 4, 2, 7, 0x4D435054, 1, 10.0),   # C4: 70k tris, depth-32 KD, global variant
 ]
 
 
@@ -37,7 +38,7 @@ def _oracle_render(oracle_mod, scene_path, W, H, spp, chunk, depth, seed, fkd, i
 def test_image_and_counters_match_oracle(mcpt, oracle_mod, case):
     sc, W, H, spp, chunk, depth, seed, fkd, illum = case
     path = mcpt.scene_path(sc)
-    scene_id = 1 if sc == "scene01" else 2
+    scene_id = 2 if sc in ("scene02", "scene03") else 1
     ref, rc = _oracle_render(oracle_mod, path, W, H, spp, chunk, depth, seed, fkd, illum, scene_id)
     scene = mcpt.Scene(mcpt.ObjModel(path))
     p = mcpt.RenderParams.for_scene(scene_id, width=W, height=H, spp=spp, spp_chunk=chunk, max_depth=depth,
