@@ -74,6 +74,8 @@ def main():
     ap.add_argument("--height", type=int, default=1024)
     ap.add_argument("--spp", type=int, default=1024)
     ap.add_argument("--spp-chunk", type=int, default=32)
+    ap.add_argument("--pipeline", choices=["megakernel", "wavefront"], default="megakernel")
+    ap.add_argument("--wf-batch", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -96,7 +98,7 @@ def main():
     scene_id = 2 if args.scene in ("scene02", "scene03") else 1
     p = M.RenderParams.for_scene(scene_id, width=args.width, height=args.height, spp=args.spp,
                                  spp_chunk=args.spp_chunk, tile=8, shard_count=world, shard_index=rank,
-                                 packed=world > 1)
+                                 packed=world > 1, pipeline=args.pipeline, wf_batch=args.wf_batch)
     n_out = p.output_pixels()
     fb = torch.zeros((n_out, 4), dtype=torch.float32, device=dev)
     scene.reserve(p)
@@ -160,7 +162,8 @@ def main():
             "config": {"workload": f"cornell_{args.width}x{args.height}_{args.spp}spp", "scene": args.scene,
                        "width": args.width, "height": args.height, "spp": args.spp, "max_depth": 7,
                        "spp_chunk": args.spp_chunk, "parallelism": f"pixel-tiles x{world}" +
-                       (" + rccl gather" if world > 1 else ""), "kernel_variant": st["variant"]},
+                       (" + rccl gather" if world > 1 else ""), "pipeline": args.pipeline,
+                       "kernel_variant": st["variant"]},
             "rays_per_step": rays // args.steps,
             "rays_per_path": round(st["rays"] / max(st["paths"], 1), 4),
             "stack_spills_per_ray": round(st["stack_spills"] / max(st["rays"], 1), 4),

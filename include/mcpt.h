@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define MCPT_ABI_VERSION 1
+#define MCPT_ABI_VERSION 2
 
 enum {
     MCPT_OK = 0,
@@ -83,7 +83,14 @@ typedef struct {
     int32_t shard_count;        /* tiles t with t % shard_count == shard_index are rendered; 0/1 = all */
     int32_t shard_index;
     int32_t packed;             /* 1: write owned tiles packed (tile-major) instead of row-major */
+    int32_t pipeline;           /* MCPT_PIPELINE_*: megakernel (default) or wavefront; same image */
+    uint32_t wf_batch;          /* wavefront: max paths in flight per batch, 0 = 1<<24 */
 } mcpt_render_params;
+
+enum {
+    MCPT_PIPELINE_MEGAKERNEL = 0,   /* one persistent kernel per render (render.hip) */
+    MCPT_PIPELINE_WAVEFRONT = 1     /* generate / extend / shade / accumulate queues (wavefront.hip) */
+};
 
 typedef struct {
     uint64_t rays;              /* closest-hit queries */
@@ -97,7 +104,8 @@ typedef struct {
     uint64_t renders;           /* render calls covered by this record */
     double kernel_ms;           /* summed GPU time of the path kernel */
     double reduce_ms;           /* summed GPU time of the partial-sum reduction */
-    int32_t variant;            /* kernel variant of the last call (1,2: scene in LDS; 3: global) */
+    int32_t variant;            /* variant of the last call: megakernel 1,2 scene in LDS, 3 global;
+                                   wavefront 4 scene in LDS, 5 global */
     int32_t pad_;
 } mcpt_render_stats;
 

@@ -21,6 +21,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MCPT_LIB_PATH") or os.path.join(_HERE, "lib", "libmcpt.so")
 
 MCPT_OK = 0
+ABI_VERSION = 2
+PIPELINE_MEGAKERNEL = 0
+PIPELINE_WAVEFRONT = 1
 ERRORS = {-1: "INVALID", -2: "IO", -3: "PARSE", -4: "DEVICE", -5: "NOMEM", -6: "UNSUPPORTED"}
 
 
@@ -48,6 +51,7 @@ class RenderParamsC(C.Structure):
         ("eye", C.c_float * 3), ("dir", C.c_float * 3), ("up", C.c_float * 3),
         ("seed", C.c_uint64), ("prev_count", C.c_uint32), ("fresnel_kd", C.c_int32),
         ("tile", C.c_int32), ("shard_count", C.c_int32), ("shard_index", C.c_int32), ("packed", C.c_int32),
+        ("pipeline", C.c_int32), ("wf_batch", C.c_uint32),
     ]
 
 
@@ -121,7 +125,7 @@ def lib():
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
-        if L.mcpt_abi_version() != 1:
+        if L.mcpt_abi_version() != ABI_VERSION:
             raise ImportError("libmcpt.so ABI version mismatch")
         _lib = L
     return _lib

@@ -7,6 +7,7 @@
 // every call takes the opaque handle it works on.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cfloat>
 #include <cmath>
 #include <cstdio>
@@ -82,6 +83,8 @@ struct Workspace {
     size_t spill_bytes = 0;
     void* fb = nullptr;          // mcpt_render staging framebuffer
     size_t fb_bytes = 0;
+    void* wf = nullptr;          // wavefront queues / path state (one allocation)
+    size_t wf_bytes = 0;
 };
 
 struct Timing {
@@ -110,7 +113,7 @@ struct mcpt_scene {
         (void)hipGetDevice(&prev);
         (void)hipSetDevice(device);
         (void)hipDeviceSynchronize();
-        for (void* p : {d_image, d_normals, ws.partial, ws.small, ws.spill, ws.fb})
+        for (void* p : {d_image, d_normals, ws.partial, ws.small, ws.spill, ws.fb, ws.wf})
             if (p) (void)hipFree(p);
         for (auto& t : pending) for (auto ev : t.e) (void)hipEventDestroy(ev);
         for (auto& t : free_timing) for (auto ev : t.e) (void)hipEventDestroy(ev);
@@ -196,6 +199,8 @@ void ensure_buf(void*& p, size_t& have, size_t need) {
 struct Plan {
     mcpt::KernelParams kp;
     size_t out_pixels;
+    int pipeline;
+    uint32_t wf_capacity;        // paths per wavefront batch
 };
 
 Plan make_plan(const mcpt_scene& s, const mcpt_render_params* p) {
@@ -249,6 +254,15 @@ Plan make_plan(const mcpt_scene& s, const mcpt_render_params* p) {
         k.ready_thresh = th < 1 ? 1 : (th > 64 ? 64 : th);
     }
     pl.out_pixels = k.packed ? size_t(npix) : size_t(p->width) * size_t(p->height);
+    if (p->pipeline != MCPT_PIPELINE_MEGAKERNEL && p->pipeline != MCPT_PIPELINE_WAVEFRONT)
+        throw mcpt::Error{MCPT_E_INVALID, "unknown pipeline"};
+    pl.pipeline = p->pipeline;
+    {
+        uint64_t cap = p->wf_batch ? p->wf_batch : (1u << 24);
+        cap = std::max<uint64_t>(cap, chunk);                        // at least one pixel per batch
+        cap = std::min<uint64_t>(cap, std::max<uint64_t>(npix, 1) * chunk);
+        pl.wf_capacity = static_cast<uint32_t>(cap);
+    }
     return pl;
 }
 
@@ -264,6 +278,33 @@ void prepare_workspace(mcpt_scene& s, mcpt::KernelParams& k) {
     k.counter = static_cast<uint32_t*>(s.ws.small);
     k.stats = reinterpret_cast<unsigned long long*>(static_cast<char*>(s.ws.small) + 64);
     k.spill = static_cast<uint4*>(s.ws.spill);
+}
+
+// wavefront workspace: 2 ray queues (o, d float4), hits, 4 class lists,
+// path state and radiance, per-bounce counters -- carved from one buffer
+mcpt::WfParams prepare_wavefront(mcpt_scene& s, const Plan& pl) {
+    const size_t cap = pl.wf_capacity;
+    const size_t bounces = size_t(pl.kp.max_depth) + 2;
+    const size_t f4 = cap * 16;
+    const size_t need = 4 * f4 + f4 + 4 * cap * 4 + 2 * f4 + bounces * sizeof(mcpt::WfCounters) + 256;
+    ensure_buf(s.ws.wf, s.ws.wf_bytes, need);
+    char* b = static_cast<char*>(s.ws.wf);
+    mcpt::WfParams w;
+    std::memset(&w, 0, sizeof w);
+    w.q_o[0] = reinterpret_cast<float4*>(b); b += f4;
+    w.q_o[1] = reinterpret_cast<float4*>(b); b += f4;
+    w.q_d[0] = reinterpret_cast<float4*>(b); b += f4;
+    w.q_d[1] = reinterpret_cast<float4*>(b); b += f4;
+    w.hit = reinterpret_cast<float4*>(b); b += f4;
+    w.pstate = reinterpret_cast<float4*>(b); b += f4;
+    w.radiance = reinterpret_cast<float4*>(b); b += f4;
+    w.cls_list = reinterpret_cast<uint32_t*>(b); b += 4 * cap * 4;
+    w.cnt = reinterpret_cast<mcpt::WfCounters*>(b);
+    w.capacity = static_cast<uint32_t>(cap);
+    const char* e = std::getenv("MCPT_WF_REFILL");
+    const int th = e ? std::atoi(e) : 16;
+    w.refill_thresh = th < 1 ? 1 : (th > 64 ? 64 : th);
+    return w;
 }
 
 void set_device(const mcpt_scene& s) {
@@ -287,8 +328,15 @@ void render_async(mcpt_scene& s, const mcpt_render_params* p, float* d_fb, hipSt
     } else {
         for (auto& ev : t.e) HIP_TRY(hipEventCreate(&ev));
     }
-    HIP_TRY(mcpt::launch_render(pl.kp, s.cus, st, t.e[0], t.e[1], t.e[2], reinterpret_cast<float4*>(d_fb),
-                                &s.last_variant));
+    if (pl.pipeline == MCPT_PIPELINE_WAVEFRONT) {
+        if (d_unit_counters) throw mcpt::Error{MCPT_E_UNSUPPORTED, "unit counters need the megakernel pipeline"};
+        const mcpt::WfParams wf = prepare_wavefront(s, pl);
+        HIP_TRY(mcpt::launch_wavefront(pl.kp, wf, s.cus, pl.kp.max_depth + 1, st, t.e[0], t.e[1], t.e[2],
+                                       reinterpret_cast<float4*>(d_fb), &s.last_variant));
+    } else {
+        HIP_TRY(mcpt::launch_render(pl.kp, s.cus, st, t.e[0], t.e[1], t.e[2], reinterpret_cast<float4*>(d_fb),
+                                    &s.last_variant));
+    }
     s.pending.push_back(t);
     s.renders++;
 }
@@ -662,6 +710,7 @@ int mcpt_scene_reserve(mcpt_scene* s, const mcpt_render_params* p) {
         set_device(*s);
         Plan pl = make_plan(*s, p);
         prepare_workspace(*s, pl.kp);
+        if (pl.pipeline == MCPT_PIPELINE_WAVEFRONT) (void)prepare_wavefront(*s, pl);
         return MCPT_OK;
     });
 }

@@ -64,10 +64,41 @@ struct KernelParams {
     int32_t ready_thresh;                // lanes ready before a shading round (1..64)
 };
 
+// Wavefront pipeline workspace (wavefront.hip).  One batch = samples
+// [s_begin, s_begin + ns) of chunk `chunk` for owned pixels [v0, v0 + nb);
+// path id pid = s_local * nb + (v - v0).  Queues are indexed by slot, path
+// state and radiance by pid.
+struct WfCounters {                      // per bounce b (ray query index), 16 words
+    uint32_t queued;                     // rays in queue b (appended by generate / shade b-1)
+    uint32_t fetched;                    // extend b work counter
+    uint32_t cls[4];                     // slots per class after extend b
+    uint32_t taken[4];                   // shade b work counters per class
+    uint32_t pad[6];
+};
+struct WfParams {
+    float4* q_o[2];                      // ray origin .xyz, pid bits in .w          [capacity]
+    float4* q_d[2];                      // ray direction .xyz, depth bits in .w     [capacity]
+    float4* hit;                         // (t, beta, gamma, htri bits) per slot     [capacity]
+    uint32_t* cls_list;                  // [4][capacity] slots per material class
+    float4* pstate;                      // (throughput .xyz, rng state bits) per pid [capacity]
+    float4* radiance;                    // path radiance per pid                   [capacity]
+    WfCounters* cnt;                     // [max_depth + 2]
+    uint32_t capacity;
+    uint32_t v0, nb, s_begin, ns, chunk_index;
+    int32_t bounce;
+    int32_t refill_thresh;               // idle lanes before an extend wave refills
+};
+
 size_t lds_bytes_in_lds(uint32_t image_bytes, int S);
 int total_lanes_for(uint32_t image_bytes, int cus);
 // memset counter, path kernel (events ev0/ev1 around it), reduce kernel (ev2)
 hipError_t launch_render(const KernelParams& kp, int cus, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1,
                          hipEvent_t ev2, float4* fb, int* variant_out);
+hipError_t launch_reduce(const KernelParams& kp, float4* fb, hipStream_t st);
+// wavefront pipeline: generate / extend / shade per bounce / accumulate per
+// batch, then the same reduction (events: ev0 before, ev1 after the batches)
+hipError_t launch_wavefront(const KernelParams& kp, const WfParams& wf, int cus, int max_bounces,
+                            hipStream_t st, hipEvent_t ev0, hipEvent_t ev1, hipEvent_t ev2, float4* fb,
+                            int* variant_out);
 
 }  // namespace mcpt

@@ -143,6 +143,9 @@ class ObjModel:
         return out
 
 
+PIPELINES = {"megakernel": _capi.PIPELINE_MEGAKERNEL, "wavefront": _capi.PIPELINE_WAVEFRONT}
+
+
 @dataclass
 class RenderParams:
     """Render configuration; defaults are the CVMCTracer constants for scene 1."""
@@ -164,6 +167,8 @@ class RenderParams:
     shard_count: int = 1
     shard_index: int = 0
     packed: bool = False
+    pipeline: str = "megakernel"      # or "wavefront" (C5): identical image, different kernels
+    wf_batch: int = 0                 # wavefront paths in flight per batch, 0 = 1<<24
 
     @staticmethod
     def for_scene(scene_id: int, **kw) -> "RenderParams":
@@ -184,6 +189,10 @@ class RenderParams:
         p.fresnel_kd = 1 if self.fresnel_kd else 0
         p.tile, p.shard_count, p.shard_index = int(self.tile), int(self.shard_count), int(self.shard_index)
         p.packed = 1 if self.packed else 0
+        if self.pipeline not in PIPELINES:
+            raise ValueError(f"pipeline must be one of {sorted(PIPELINES)}")
+        p.pipeline = PIPELINES[self.pipeline]
+        p.wf_batch = int(self.wf_batch)
         return p
 
     def output_pixels(self) -> int:

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol(mcpt):
 
 def test_abi_version_and_defaults(mcpt):
     from montecarlopathtracer_amd._capi import RenderParamsC, lib
-    assert lib().mcpt_abi_version() == 1
+    assert lib().mcpt_abi_version() == 2
     p = RenderParamsC()
     lib().mcpt_render_params_default(C.byref(p))
     # CV/stdafx.h:41-46, CUTracer.cu:189,212,349-351
@@ -75,3 +75,30 @@ def test_pw_tracer_adapter_compiles_and_links(mcpt):
     sys.path.insert(0, os.path.join(ROOT, "tests", "cpp"))
     import build_dropin
     assert os.path.exists(build_dropin.build())
+
+
+def test_struct_layouts_match_header(mcpt, tmp_path):
+    """ctypes mirrors (_capi.py) have the sizes and field offsets of include/mcpt.h."""
+    import ctypes
+    import subprocess
+    from montecarlopathtracer_amd import _capi
+    inc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
+    structs = {"mcpt_render_params": _capi.RenderParamsC, "mcpt_render_stats": _capi.RenderStats,
+               "mcpt_scene_info": _capi.SceneInfo, "mcpt_model_info": _capi.ModelInfo,
+               "mcpt_model_desc": _capi.ModelDesc}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "mcpt.h"', 'int main(void) {']
+    for cname, py in structs.items():
+        lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')
+        for f, _ in py._fields_:
+            lines.append(f'printf("{cname}.{f} %zu\\n", offsetof({cname}, {f}));')
+    lines.append("return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c99", "-I", inc, str(src), "-o", str(exe)], check=True)
+    out = dict(l.rsplit(" ", 1) for l in subprocess.run([str(exe)], capture_output=True, text=True,
+                                                         check=True).stdout.split("\n") if l)
+    for cname, py in structs.items():
+        assert int(out[cname]) == ctypes.sizeof(py), cname
+        for f, _ in py._fields_:
+            assert int(out[f"{cname}.{f}"]) == getattr(py, f).offset, (cname, f)

@@ -34,16 +34,18 @@ def _oracle_render(oracle_mod, scene_path, W, H, spp, chunk, depth, seed, fkd, i
     return o.render(p, out)
 
 
+@pytest.mark.parametrize("pipeline", ["megakernel", "wavefront"])
 @pytest.mark.parametrize("case", CASES, ids=[f"{c[0]}-{c[1]}x{c[2]}-spp{c[3]}-d{c[5]}" for c in CASES])
-def test_image_and_counters_match_oracle(mcpt, oracle_mod, case):
+def test_image_and_counters_match_oracle(mcpt, oracle_mod, case, pipeline):
     sc, W, H, spp, chunk, depth, seed, fkd, illum = case
     path = mcpt.scene_path(sc)
     scene_id = 2 if sc in ("scene02", "scene03") else 1
     ref, rc = _oracle_render(oracle_mod, path, W, H, spp, chunk, depth, seed, fkd, illum, scene_id)
     scene = mcpt.Scene(mcpt.ObjModel(path))
     p = mcpt.RenderParams.for_scene(scene_id, width=W, height=H, spp=spp, spp_chunk=chunk, max_depth=depth,
-                                    seed=seed, fresnel_kd=bool(fkd), illum=illum)
+                                    seed=seed, fresnel_kd=bool(fkd), illum=illum, pipeline=pipeline)
     img, st = scene.render(p)
+    assert st["variant"] in ((1, 2, 3) if pipeline == "megakernel" else (4, 5))
     rmse = float(np.sqrt(np.mean((img - ref) ** 2)))
     assert rmse < 1e-4
     assert np.array_equal(img, ref), f"max abs diff {np.abs(img - ref).max()}, equal frac {(img == ref).mean()}"
@@ -116,3 +118,18 @@ def test_pw_tracer_adapter_matches_abi(mcpt, tmp_path):
     host = np.zeros((30, 40, 3), np.float32)
     tr.render_scene(1, host, num_kernels=3, samples_per_kernel=4)
     assert np.array_equal(got, host)
+
+
+@pytest.mark.parametrize("batch", [1000, 4096, 0])
+def test_wavefront_batches_equal_megakernel(mcpt, batch):
+    """Any batch split of the wavefront (partial batches, ragged last chunk,
+    shards) renders the megakernel's image and counts bit for bit."""
+    path = mcpt.scene_path("scene01")
+    scene = mcpt.Scene(mcpt.ObjModel(path))
+    for kw in ({"width": 61, "height": 45, "spp": 7, "spp_chunk": 3},
+               {"width": 64, "height": 64, "spp": 5, "spp_chunk": 5, "shard_count": 3, "shard_index": 1}):
+        mk, smk = scene.render(mcpt.RenderParams(**kw))
+        wf, swf = scene.render(mcpt.RenderParams(pipeline="wavefront", wf_batch=batch, **kw))
+        assert np.array_equal(mk, wf)
+        for k in ("rays", "paths", "inner_visits", "leaf_visits", "leaf_refs", "tri_tests", "shades"):
+            assert smk[k] == swf[k], (k, smk[k], swf[k])
