@@ -3,16 +3,19 @@
 //
 // Same paths, same arithmetic as the megakernel (render.hip), reorganised as
 // queues in HBM so that every kernel does one kind of work:
-//   generate    one primary ray per (pixel, sample) of the batch, appended to
-//               ray queue 0 (wave ballot + prefix compaction, one atomic/wave)
+//   generate    one primary ray per (pixel, sample) of the batch into ray
+//               queue 0 at slot = path id
 //   extend b    closest hit of every ray in queue b: persistent workgroups,
-//               scene image in LDS (or global), lanes refill from the queue as
-//               soon as their ray is done; the slot is appended to one of four
-//               per-class lists (terminate / diffuse / phong / fresnel) -- the
-//               material sort of the extend -> shade hand-off
-//   shade b     one class list after another, so each wave runs ONE material
-//               branch: radiance of terminated paths, or the scatter event and
-//               the next ray appended (compacted) to queue b+1
+//               scene image in LDS (or global); each wave reserves queue
+//               slots 64 at a time, each lane prefetches its next ray while
+//               tracing the current one and refills as soon as it is done;
+//               the slot then goes to one of four per-class lists (terminate /
+//               diffuse / phong / fresnel) -- the material sort of the
+//               extend -> shade hand-off -- buffered 64 entries per class in
+//               registers (ds_permute) and written with one atomic per block
+//   shade b     the class lists back to back, so each wave runs ONE material
+//               branch: radiance of terminated paths, or the scatter event
+//               whose next ray goes to slot i of queue b+1 (dense, no atomics)
 //   accumulate  per pixel, the batch's samples summed in sample order into the
 //               same [chunk][pixel] partial sums the megakernel writes
 // followed by the megakernel's reduction.  The RNG is stateless per
@@ -42,42 +45,107 @@ constexpr int kClassTerminate = 0;
 __device__ __forceinline__ float4 pack(V3 v, uint32_t w) { return make_float4(v.x, v.y, v.z, __uint_as_float(w)); }
 __device__ __forceinline__ V3 xyz(float4 v) { return v3(v.x, v.y, v.z); }
 
+// Rays are carried as (o.xyz, pid) and (d.xyz, depth); depth kNoRay marks a
+// queue slot without a ray (pixel outside the image): it ends as a miss with
+// zero radiance and is counted nowhere, like the megakernel's empty units.
+constexpr uint32_t kNoRay = 0xFFFFFFFFu;
+constexpr uint32_t kChunk = 64;           // queue slots a wave reserves at once
+
 // ---- generate: primary rays of the batch (CUTracer.cu:186-211) -------------
+// queue slot = path id, no atomics
 __global__ void __launch_bounds__(kGenBlock) wf_generate(const KernelParams kp, const WfParams wf) {
     const uint32_t n = wf.nb * wf.ns;
     const V3 eye = v3(kp.eye[0], kp.eye[1], kp.eye[2]);
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0};
-    const uint32_t stride = gridDim.x * kGenBlock;
-    // wave-uniform trip count: every lane of a wave runs each iteration
-    const uint32_t wave0 = (blockIdx.x * kGenBlock + threadIdx.x) & ~63u;
-    for (uint32_t base = wave0; base < n; base += stride) {
-        const uint32_t pid = base + (threadIdx.x & 63u);
-        bool ok = false;
+    if (blockIdx.x == 0 && threadIdx.x == 0) wf.cnt[0].queued = n;
+    for (uint32_t pid = blockIdx.x * kGenBlock + threadIdx.x; pid < n; pid += gridDim.x * kGenBlock) {
+        const uint32_t s_local = pid / wf.nb;
+        const uint32_t v = wf.v0 + (pid - s_local * wf.nb);
+        int px, py;
         V3 d = v3(0, 0, 0);
-        if (pid < n) {
-            const uint32_t s_local = pid / wf.nb;
-            const uint32_t v = wf.v0 + (pid - s_local * wf.nb);
-            int px, py;
-            if (unit_pixel(kp, v, px, py)) {
-                uint32_t sd;
-                const uint32_t pix = (uint32_t)py * (uint32_t)kp.width + (uint32_t)px;
-                primary_ray(kp, pix, px, py, wf.s_begin + s_local, sd, d);
-                wf.pstate[pid] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(sd));
-                c.paths++;
-                c.rays++;
-                ok = true;
-            } else {
-                wf.radiance[pid] = make_float4(0, 0, 0, 0);
-            }
+        uint32_t depth = kNoRay;
+        if (unit_pixel(kp, v, px, py)) {
+            uint32_t sd;
+            const uint32_t pix = (uint32_t)py * (uint32_t)kp.width + (uint32_t)px;
+            primary_ray(kp, pix, px, py, wf.s_begin + s_local, sd, d);
+            wf.pstate[pid] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(sd));
+            c.paths++;
+            c.rays++;
+            depth = 0;
         }
-        const uint32_t slot = wave_append(ok, &wf.cnt[0].queued);
-        if (ok) {
-            wf.q_o[0][slot] = pack(eye, pid);
-            wf.q_d[0][slot] = pack(d, 0u);
-        }
+        wf.q_o[0][pid] = pack(eye, pid);
+        wf.q_d[0][pid] = pack(d, depth);
     }
     flush_counters(c, kp.stats);
 }
+
+// Wave-level slot reservation: lanes with `want` get consecutive queue slots
+// from the wave's current 64-slot chunk, one atomic per 64 slots.
+struct SlotCursor {
+    uint32_t base, used;
+    __device__ __forceinline__ uint32_t take(bool want, uint32_t* counter) {
+        const uint64_t m = __ballot(want);
+        const uint32_t n = (uint32_t)__popcll(m);
+        const int lane = (int)(threadIdx.x & 63u);
+        const uint32_t rank = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        uint32_t res = base + used + rank;
+        if (used + n > kChunk) {                       // wave-uniform
+            const uint32_t first = kChunk - used;
+            uint32_t nb = 0;
+            if (lane == 0) nb = atomicAdd(counter, kChunk);
+            nb = __shfl(nb, 0);
+            if (rank >= first) res = nb + (rank - first);
+            base = nb;
+            used = n - first;
+        } else {
+            used += n;
+        }
+        return res;
+    }
+};
+
+// Per-class output buffer held in registers: lane j holds entry j of the
+// wave's pending 64-entry block; full blocks go out with one atomic and one
+// coalesced store.  Entries move to their lane with ds_permute (all 64 lanes
+// send: appenders to the new positions, the others to the remaining lanes, so
+// the permutation has no collisions).
+struct ClassBuf {
+    uint32_t val, count;
+    __device__ __forceinline__ void append(bool want, uint32_t x, uint32_t* counter, uint32_t* list) {
+        const uint64_t m = __ballot(want);
+        const uint32_t n = (uint32_t)__popcll(m);
+        if (n == 0) return;                           // wave-uniform
+        const int lane = (int)(threadIdx.x & 63u);
+        const uint64_t lt = (1ull << lane) - 1ull;
+        const uint32_t pos = want ? (uint32_t)__popcll(m & lt) : n + (uint32_t)__popcll(~m & lt);
+        const uint32_t dst = (count + pos) & 63u;
+        const uint32_t recv = (uint32_t)__builtin_amdgcn_ds_permute((int)(dst << 2), (int)x);
+        const uint32_t off = ((uint32_t)lane - count) & 63u;
+        const bool mine = off < n;
+        const uint32_t hi = count + n;
+        if (hi < kChunk) {
+            if (mine) val = recv;
+            count = hi;
+        } else {
+            if (mine && (uint32_t)lane >= count) val = recv;
+            uint32_t b = 0;
+            if (lane == 0) b = atomicAdd(counter, kChunk);
+            b = __shfl(b, 0);
+            list[b + (uint32_t)lane] = val;
+            if (mine && (uint32_t)lane < count) val = recv;
+            count = hi - kChunk;
+        }
+    }
+    __device__ __forceinline__ void flush(uint32_t* counter, uint32_t* list) {
+        if (count == 0) return;
+        const int lane = (int)(threadIdx.x & 63u);
+        uint32_t b = 0;
+        if (lane == 0) b = atomicAdd(counter, count);
+        b = __shfl(b, 0);
+        if ((uint32_t)lane < count) list[b + (uint32_t)lane] = val;
+        count = 0;
+    }
+};
 
 // ---- extend: closest hit of every queued ray --------------------------------
 template <bool IN_LDS, int S, int BLOCK>
@@ -115,26 +183,28 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
     const float4* qd = wf.q_d[wf.bounce & 1];
 
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0};
+    SlotCursor cur_chunk = {0, kChunk};
+    ClassBuf out[4] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
     RayState r;
     r.htri = -1;
-    int mode = kNeed;
-    uint32_t slot = 0, depth = 0;
-    for (;;) {
-        // ---- refill idle lanes from the queue (one atomic per wave) ---------
-        const uint32_t got = wave_append(mode == kNeed, &cn->fetched);
-        if (mode == kNeed) {
-            if (got >= count) {
-                mode = kDead;
-            } else {
-                slot = got;
-                const float4 o4 = qo[slot], d4 = qd[slot];
-                r.o = xyz(o4);
-                r.d = xyz(d4);
-                depth = __float_as_uint(d4.w);
-                mode = begin_ray(r, sc) ? kTrav : kReady;
-            }
+    int mode = kDead;
+    uint32_t slot = cur_chunk.take(true, &cn->fetched), depth = 0;
+    uint32_t nslot = cur_chunk.take(true, &cn->fetched);
+    float4 no4 = make_float4(0, 0, 0, 0), nd4 = make_float4(0, 0, 0, 0);
+    auto start = [&](float4 o4, float4 d4) {
+        r.o = xyz(o4);
+        r.d = xyz(d4);
+        depth = __float_as_uint(d4.w);
+        if (depth == kNoRay) {
+            r.htri = -1;
+            mode = kReady;
+        } else {
+            mode = begin_ray(r, sc) ? kTrav : kReady;
         }
-        if (!__ballot(mode != kDead)) break;
+    };
+    if (slot < count) start(qo[slot], qd[slot]);
+    if (nslot < count) { no4 = qo[nslot]; nd4 = qd[nslot]; }
+    for (;;) {
         // ---- traversal burst until enough lanes are done ---------------------
         for (;;) {
             if (mode == kTrav) {
@@ -145,26 +215,45 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
             if (!trv || __popcll(rdy) >= wf.refill_thresh) break;
         }
         // ---- hand-off: hit record + per-material class list -----------------
+        const bool fin = mode == kReady;
         uint32_t cls = 4u;
-        if (mode == kReady) {
+        if (fin) {
             wf.hit[slot] = make_float4(r.best, r.hbeta, r.hgamma, __int_as_float(r.htri));
             cls = kClassTerminate;
-            if (r.htri >= 0 && (int32_t)depth < kp.max_depth) {
+            if (r.htri >= 0 && depth != kNoRay && (int32_t)depth < kp.max_depth) {
                 const GpuGeom& g = geoms[__float_as_uint(tris[3 * r.htri + 1].w)];
                 if (!is_emitter(g)) cls = material_class(g);
             }
-            mode = kNeed;
         }
 #pragma unroll
-        for (uint32_t k = 0; k < 4; k++) {
-            const uint32_t at = wave_append(cls == k, &cn->cls[k]);
-            if (cls == k) wf.cls_list[(size_t)k * wf.capacity + at] = slot;
+        for (uint32_t k = 0; k < 4; k++)
+            out[k].append(cls == k, slot, &cn->cls[k], wf.cls_list + (size_t)k * wf.capacity);
+        // ---- finished lanes start their prefetched ray, prefetch another ------
+        if (fin) {
+            if (nslot < count) {
+                slot = nslot;
+                start(no4, nd4);
+            } else {
+                mode = kDead;
+            }
         }
+        const bool want = fin && mode != kDead;
+        const uint32_t ns = cur_chunk.take(want, &cn->fetched);
+        if (want) {
+            nslot = ns;
+            if (nslot < count) { no4 = qo[nslot]; nd4 = qd[nslot]; }
+        }
+        if (!__ballot(mode != kDead)) break;
     }
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) out[k].flush(&cn->cls[k], wf.cls_list + (size_t)k * wf.capacity);
     flush_counters(c, kp.stats);
 }
 
-// ---- shade: one material class after another (CUTracer.cu:105-175) ----------
+// ---- shade: the class lists back to back (CUTracer.cu:105-175) -------------
+// Items are taken in the order [diffuse, phong, fresnel, terminate]; the i-th
+// continuing item writes its next ray to slot i of queue b+1 (no atomics), so
+// consecutive waves shade one material each.
 __global__ void __launch_bounds__(kShadeBlock) wf_shade(const KernelParams kp, const WfParams wf) {
     WfCounters* cn = wf.cnt + wf.bounce;
     WfCounters* nx = cn + 1;
@@ -175,53 +264,37 @@ __global__ void __launch_bounds__(kShadeBlock) wf_shade(const KernelParams kp, c
     const float4* qd = wf.q_d[wf.bounce & 1];
     float4* qo2 = wf.q_o[(wf.bounce + 1) & 1];
     float4* qd2 = wf.q_d[(wf.bounce + 1) & 1];
-    const int lane = (int)(threadIdx.x & 63u);
+    const uint32_t p1 = cn->cls[1], p2 = p1 + cn->cls[2], p3 = p2 + cn->cls[3], total = p3 + cn->cls[0];
+    if (blockIdx.x == 0 && threadIdx.x == 0) nx->queued = p3;
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (uint32_t k = 0; k < 4; k++) {
-        const uint32_t n = cn->cls[k];
-        const uint32_t* list = wf.cls_list + (size_t)k * wf.capacity;
-        for (;;) {
-            uint32_t base = 0;
-            if (lane == 0) base = atomicAdd(&cn->taken[k], 64u);
-            base = __shfl(base, 0);
-            if (base >= n) break;
-            const uint32_t i = base + (uint32_t)lane;
-            bool cont = false;
-            float4 o_next = make_float4(0, 0, 0, 0), d_next = make_float4(0, 0, 0, 0);
-            if (i < n) {
-                const uint32_t slot = list[i];
-                const float4 o4 = qo[slot], d4 = qd[slot], h = wf.hit[slot];
-                const uint32_t pid = __float_as_uint(o4.w);
-                const uint32_t depth = __float_as_uint(d4.w);
-                const int32_t htri = __float_as_int(h.w);
-                const float4 ps = wf.pstate[pid];
-                V3 color = xyz(ps);
-                if (k == kClassTerminate) {
-                    // miss -> 0; emitter -> color*Ka*ILLUM (:111-113); terminal query (:162-175)
-                    V3 L = v3(0, 0, 0);
-                    if (htri >= 0) {
-                        const GpuGeom& g = geoms[__float_as_uint(tris[3 * htri + 1].w)];
-                        if ((int32_t)depth >= kp.max_depth || is_emitter(g)) L = emitted(color, g, kp.illum);
-                    }
-                    wf.radiance[pid] = make_float4(L.x, L.y, L.z, 0.0f);
-                } else {
-                    c.shades++;
-                    const GpuGeom& g = geoms[__float_as_uint(tris[3 * htri + 1].w)];
-                    uint32_t sd = __float_as_uint(ps.w);
-                    V3 o = xyz(o4), d = xyz(d4);
-                    scatter(g, sc.normals, htri, h.y, h.z, h.x, kp.fresnel_kd, sd, color, o, d);
-                    wf.pstate[pid] = pack(color, sd);
-                    o_next = pack(o, pid);
-                    d_next = pack(d, depth + 1u);
-                    c.rays++;
-                    cont = true;
-                }
+    for (uint32_t i = blockIdx.x * kShadeBlock + threadIdx.x; i < total; i += gridDim.x * kShadeBlock) {
+        const uint32_t k = i < p1 ? 1u : (i < p2 ? 2u : (i < p3 ? 3u : 0u));
+        const uint32_t start = k == 1u ? 0u : (k == 2u ? p1 : (k == 3u ? p2 : p3));
+        const uint32_t slot = wf.cls_list[(size_t)k * wf.capacity + (i - start)];
+        const float4 o4 = qo[slot], d4 = qd[slot], h = wf.hit[slot];
+        const uint32_t pid = __float_as_uint(o4.w);
+        const uint32_t depth = __float_as_uint(d4.w);
+        const int32_t htri = __float_as_int(h.w);
+        if (k == kClassTerminate) {
+            // miss -> 0; emitter -> color*Ka*ILLUM (:111-113); terminal query (:162-175)
+            V3 L = v3(0, 0, 0);
+            if (htri >= 0 && depth != kNoRay) {
+                const GpuGeom& g = geoms[__float_as_uint(tris[3 * htri + 1].w)];
+                if ((int32_t)depth >= kp.max_depth || is_emitter(g)) L = emitted(xyz(wf.pstate[pid]), g, kp.illum);
             }
-            const uint32_t at = wave_append(cont, &nx->queued);
-            if (cont) {
-                qo2[at] = o_next;
-                qd2[at] = d_next;
-            }
+            wf.radiance[pid] = make_float4(L.x, L.y, L.z, 0.0f);
+        } else {
+            c.shades++;
+            const float4 ps = wf.pstate[pid];
+            V3 color = xyz(ps);
+            const GpuGeom& g = geoms[__float_as_uint(tris[3 * htri + 1].w)];
+            uint32_t sd = __float_as_uint(ps.w);
+            V3 o = xyz(o4), d = xyz(d4);
+            scatter(g, sc.normals, htri, h.y, h.z, h.x, kp.fresnel_kd, sd, color, o, d);
+            wf.pstate[pid] = pack(color, sd);
+            qo2[i] = pack(o, pid);
+            qd2[i] = pack(d, depth + 1u);
+            c.rays++;
         }
     }
     flush_counters(c, kp.stats);
@@ -271,7 +344,7 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams& wf_in, in
             if (e != hipSuccess) return e;
             const uint32_t n = wf.nb * wf.ns;
             const uint32_t gen_grid = (n + kGenBlock - 1) / kGenBlock;
-            hipLaunchKernelGGL(wf_generate, dim3(gen_grid < 8u * (uint32_t)cus ? gen_grid : 8u * (uint32_t)cus),
+            hipLaunchKernelGGL(wf_generate, dim3(gen_grid < 16u * (uint32_t)cus ? gen_grid : 16u * (uint32_t)cus),
                                dim3(kGenBlock), 0, st, kp, wf);
             if ((e = hipGetLastError()) != hipSuccess) return e;
             for (int b = 0; b < max_bounces; b++) {
