@@ -284,9 +284,11 @@ void prepare_workspace(mcpt_scene& s, mcpt::KernelParams& k) {
 // path state and radiance, per-bounce counters -- carved from one buffer
 mcpt::WfParams prepare_wavefront(mcpt_scene& s, const Plan& pl) {
     const size_t cap = pl.wf_capacity;
-    const size_t bounces = size_t(pl.kp.max_depth) + 2;
-    const size_t f4 = cap * 16;
-    const size_t need = 4 * f4 + f4 + 4 * cap * 4 + 2 * f4 + bounces * sizeof(mcpt::WfCounters) + 256;
+    const size_t bounces = (size_t(pl.kp.max_depth) + 2) * size_t(mcpt::wavefront_segments(s.gpu.image_bytes, s.cus));
+    // segments hold whole 64-path groups: up to nseg*64 slots beyond the paths
+    const size_t cap_slots = cap + size_t(mcpt::wavefront_segments(s.gpu.image_bytes, s.cus)) * 64;
+    const size_t f4 = cap_slots * 16;
+    const size_t need = 4 * f4 + f4 + 4 * cap_slots * 4 + 2 * f4 + bounces * sizeof(mcpt::WfCounters) + 256;
     ensure_buf(s.ws.wf, s.ws.wf_bytes, need);
     char* b = static_cast<char*>(s.ws.wf);
     mcpt::WfParams w;
@@ -298,9 +300,10 @@ mcpt::WfParams prepare_wavefront(mcpt_scene& s, const Plan& pl) {
     w.hit = reinterpret_cast<float4*>(b); b += f4;
     w.pstate = reinterpret_cast<float4*>(b); b += f4;
     w.radiance = reinterpret_cast<float4*>(b); b += f4;
-    w.cls_list = reinterpret_cast<uint32_t*>(b); b += 4 * cap * 4;
+    w.cls_list = reinterpret_cast<uint32_t*>(b); b += 4 * cap_slots * 4;
     w.cnt = reinterpret_cast<mcpt::WfCounters*>(b);
-    w.capacity = static_cast<uint32_t>(cap);
+    w.capacity = static_cast<uint32_t>(cap);       // paths per batch (pid range)
+    w.slot_stride = static_cast<uint32_t>(cap_slots);
     const char* e = std::getenv("MCPT_WF_REFILL");
     const int th = e ? std::atoi(e) : 16;
     w.refill_thresh = th < 1 ? 1 : (th > 64 ? 64 : th);

@@ -66,14 +66,15 @@ struct KernelParams {
 
 // Wavefront pipeline workspace (wavefront.hip).  One batch = samples
 // [s_begin, s_begin + ns) of chunk `chunk` for owned pixels [v0, v0 + nb);
-// path id pid = s_local * nb + (v - v0).  Queues are indexed by slot, path
-// state and radiance by pid.
-struct WfCounters {                      // per bounce b (ray query index), 16 words
-    uint32_t queued;                     // rays in queue b (appended by generate / shade b-1)
-    uint32_t fetched;                    // extend b work counter
-    uint32_t cls[4];                     // slots per class after extend b
-    uint32_t taken[4];                   // shade b work counters per class
-    uint32_t pad[6];
+// path id pid = s_local * nb + (v - v0).  The batch is cut into `nseg`
+// segments of `seg` paths, one per extend workgroup; a path stays in its
+// segment for all bounces, so each segment's queues, class lists and
+// counters are private to one workgroup (LDS atomics only).  Queue slot j of
+// segment g is entry g*seg + j; path state and radiance are indexed by pid.
+struct WfCounters {                      // per (bounce, segment), 8 words
+    uint32_t queued;                     // rays in this segment's queue
+    uint32_t cls[4];                     // class-list lengths after extend
+    uint32_t pad[3];
 };
 struct WfParams {
     float4* q_o[2];                      // ray origin .xyz, pid bits in .w          [capacity]
@@ -82,9 +83,11 @@ struct WfParams {
     uint32_t* cls_list;                  // [4][capacity] slots per material class
     float4* pstate;                      // (throughput .xyz, rng state bits) per pid [capacity]
     float4* radiance;                    // path radiance per pid                   [capacity]
-    WfCounters* cnt;                     // [max_depth + 2]
-    uint32_t capacity;
+    WfCounters* cnt;                     // [max_depth + 2][nseg]
+    uint32_t capacity;                   // paths per batch
+    uint32_t slot_stride;                // queue / class-list entries per array (>= nseg * seg)
     uint32_t v0, nb, s_begin, ns, chunk_index;
+    uint32_t nseg, seg;                  // segments (= extend workgroups) and paths per segment
     int32_t bounce;
     int32_t refill_thresh;               // idle lanes before an extend wave refills
 };
@@ -95,6 +98,8 @@ int total_lanes_for(uint32_t image_bytes, int cus);
 hipError_t launch_render(const KernelParams& kp, int cus, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1,
                          hipEvent_t ev2, float4* fb, int* variant_out);
 hipError_t launch_reduce(const KernelParams& kp, float4* fb, hipStream_t st);
+// wavefront queue segments (= extend workgroups) for a scene image
+int wavefront_segments(uint32_t image_bytes, int cus);
 // wavefront pipeline: generate / extend / shade per bounce / accumulate per
 // batch, then the same reduction (events: ev0 before, ev1 after the batches)
 hipError_t launch_wavefront(const KernelParams& kp, const WfParams& wf, int cus, int max_bounces,

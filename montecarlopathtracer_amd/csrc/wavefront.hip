@@ -4,25 +4,30 @@
 // Same paths, same arithmetic as the megakernel (render.hip), reorganised as
 // queues in HBM so that every kernel does one kind of work:
 //   generate    one primary ray per (pixel, sample) of the batch into ray
-//               queue 0 at slot = path id
-//   extend b    closest hit of every ray in queue b: persistent workgroups,
-//               scene image in LDS (or global); each wave reserves queue
-//               slots 64 at a time, each lane prefetches its next ray while
-//               tracing the current one and refills as soon as it is done;
-//               the slot then goes to one of four per-class lists (terminate /
-//               diffuse / phong / fresnel) -- the material sort of the
-//               extend -> shade hand-off -- buffered 64 entries per class in
-//               registers (ds_permute) and written with one atomic per block
-//   shade b     the class lists back to back, so each wave runs ONE material
-//               branch: radiance of terminated paths, or the scatter event
-//               whose next ray goes to slot i of queue b+1 (dense, no atomics)
+//               queue 0, 64-path groups (an 8x8 tile) dealt to the segments
+//               round-robin
+//   extend b    closest hit of every ray in queue b: one persistent workgroup
+//               per queue segment, scene image in LDS (or global); waves
+//               reserve slots 64 at a time from an LDS counter, each lane
+//               prefetches its next ray while tracing the current one and
+//               refills as soon as it is done; the slot then goes to one of
+//               four per-class lists (terminate / diffuse / phong / fresnel) --
+//               the material sort of the extend -> shade hand-off -- buffered
+//               64 entries per class in registers (ds_permute) and written as
+//               one coalesced block per LDS atomic
+//   shade b     each segment's class lists back to back, so each wave runs ONE
+//               material branch: radiance of terminated paths, or the scatter
+//               event whose next ray goes to slot i of the segment's queue b+1
+//               (dense, no atomics)
 //   accumulate  per pixel, the batch's samples summed in sample order into the
 //               same [chunk][pixel] partial sums the megakernel writes
-// followed by the megakernel's reduction.  The RNG is stateless per
-// (pixel, sample) and every float operation is shared (trace_device.hpp), so
-// the image is bit-identical to the megakernel's and the oracle's.  Queue
-// order is scheduling-dependent but nothing reads it: a path's state is keyed
-// by its path id.
+// followed by the megakernel's reduction.  A path never leaves its segment,
+// so no kernel touches a device-wide atomic (one shared counter serialised
+// ~0.5 M returning atomics per launch in the first version: 85% of wave
+// cycles parked).  The RNG is stateless per (pixel, sample) and every float
+// operation is shared (trace_device.hpp), so the image is bit-identical to the
+// megakernel's and the oracle's; queue order is scheduling-dependent but
+// nothing reads it: a path's state is keyed by its path id.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -41,26 +46,35 @@ namespace {
 constexpr int kGenBlock = 256;
 constexpr int kShadeBlock = 256;
 constexpr int kClassTerminate = 0;
-
-__device__ __forceinline__ float4 pack(V3 v, uint32_t w) { return make_float4(v.x, v.y, v.z, __uint_as_float(w)); }
-__device__ __forceinline__ V3 xyz(float4 v) { return v3(v.x, v.y, v.z); }
-
 // Rays are carried as (o.xyz, pid) and (d.xyz, depth); depth kNoRay marks a
 // queue slot without a ray (pixel outside the image): it ends as a miss with
 // zero radiance and is counted nowhere, like the megakernel's empty units.
 constexpr uint32_t kNoRay = 0xFFFFFFFFu;
 constexpr uint32_t kChunk = 64;           // queue slots a wave reserves at once
 
+__device__ __forceinline__ float4 pack(V3 v, uint32_t w) { return make_float4(v.x, v.y, v.z, __uint_as_float(w)); }
+__device__ __forceinline__ V3 xyz(float4 v) { return v3(v.x, v.y, v.z); }
+
 // ---- generate: primary rays of the batch (CUTracer.cu:186-211) -------------
-// queue slot = path id, no atomics
+// Paths go to segments in groups of 64 (one 8x8 tile of one sample: a
+// coherent wave of primary rays), group j -> segment j % nseg, so every
+// segment holds tiles from all over the image and the workgroups finish
+// together.
 __global__ void __launch_bounds__(kGenBlock) wf_generate(const KernelParams kp, const WfParams wf) {
     const uint32_t n = wf.nb * wf.ns;
+    const uint32_t ngroups = (n + 63u) / 64u;
     const V3 eye = v3(kp.eye[0], kp.eye[1], kp.eye[2]);
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (blockIdx.x == 0 && threadIdx.x == 0) wf.cnt[0].queued = n;
     for (uint32_t pid = blockIdx.x * kGenBlock + threadIdx.x; pid < n; pid += gridDim.x * kGenBlock) {
         const uint32_t s_local = pid / wf.nb;
         const uint32_t v = wf.v0 + (pid - s_local * wf.nb);
+        const uint32_t grp = pid >> 6, g = grp % wf.nseg;
+        const uint32_t slot = g * wf.seg + (grp / wf.nseg) * 64u + (pid & 63u);
+        if (grp < wf.nseg && (pid & 63u) == 0u) {   // first path of segment g: its queue length
+            uint32_t len = ((ngroups - g + wf.nseg - 1u) / wf.nseg) * 64u;
+            if ((ngroups - 1u) % wf.nseg == g) len -= ngroups * 64u - n;
+            wf.cnt[g].queued = len;
+        }
         int px, py;
         V3 d = v3(0, 0, 0);
         uint32_t depth = kNoRay;
@@ -73,14 +87,14 @@ __global__ void __launch_bounds__(kGenBlock) wf_generate(const KernelParams kp, 
             c.rays++;
             depth = 0;
         }
-        wf.q_o[0][pid] = pack(eye, pid);
-        wf.q_d[0][pid] = pack(d, depth);
+        wf.q_o[0][slot] = pack(eye, pid);
+        wf.q_d[0][slot] = pack(d, depth);
     }
     flush_counters(c, kp.stats);
 }
 
 // Wave-level slot reservation: lanes with `want` get consecutive queue slots
-// from the wave's current 64-slot chunk, one atomic per 64 slots.
+// from the wave's current 64-slot chunk, one LDS atomic per 64 slots.
 struct SlotCursor {
     uint32_t base, used;
     __device__ __forceinline__ uint32_t take(bool want, uint32_t* counter) {
@@ -105,10 +119,10 @@ struct SlotCursor {
 };
 
 // Per-class output buffer held in registers: lane j holds entry j of the
-// wave's pending 64-entry block; full blocks go out with one atomic and one
-// coalesced store.  Entries move to their lane with ds_permute (all 64 lanes
-// send: appenders to the new positions, the others to the remaining lanes, so
-// the permutation has no collisions).
+// wave's pending 64-entry block; full blocks go out with one LDS atomic and
+// one coalesced store.  Entries move to their lane with ds_permute (all 64
+// lanes send: appenders to the new positions, the others to the remaining
+// lanes, so the permutation has no collisions).
 struct ClassBuf {
     uint32_t val, count;
     __device__ __forceinline__ void append(bool want, uint32_t x, uint32_t* counter, uint32_t* list) {
@@ -147,15 +161,22 @@ struct ClassBuf {
     }
 };
 
-// ---- extend: closest hit of every queued ray --------------------------------
+// ---- extend: closest hit of every ray of this workgroup's segment -----------
 template <bool IN_LDS, int S, int BLOCK>
 __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const WfParams wf) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    WfCounters* cn = wf.cnt + wf.bounce;
-    const uint32_t count = cn->queued;
-    if (count == 0) return;
+    const uint32_t g = blockIdx.x;
+    WfCounters* cn = wf.cnt + (size_t)wf.bounce * wf.nseg + g;
+    const uint32_t count = g < wf.nseg ? cn->queued : 0u;
+    if (count == 0) {
+        if (g < wf.nseg && threadIdx.x < 4) cn->cls[threadIdx.x] = 0;
+        return;
+    }
     const int tid = (int)threadIdx.x;
     const GpuScene& sc = kp.scene;
+    // LDS: [scene image | stack S x BLOCK x 16 B | 5 counters]
+    uint32_t* lcnt = reinterpret_cast<uint32_t*>(smem + kp.lds_stack_off + (size_t)S * BLOCK * 16);
+    if (tid < 5) lcnt[tid] = 0;
     const float4* tris;
     const uint2* nodes;
     const uint32_t* leafs;
@@ -165,7 +186,6 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
         uint4* dst = reinterpret_cast<uint4*>(smem);
         const uint32_t n16 = sc.image_bytes / 16u;
         for (uint32_t i = (uint32_t)tid; i < n16; i += BLOCK) dst[i] = src[i];
-        __syncthreads();
         tris = reinterpret_cast<const float4*>(smem + sc.off_tris);
         nodes = reinterpret_cast<const uint2*>(smem + sc.off_nodes) + 1;
         leafs = reinterpret_cast<const uint32_t*>(smem + sc.off_leafs);
@@ -176,11 +196,14 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
         leafs = reinterpret_cast<const uint32_t*>(sc.image + sc.off_leafs);
         geoms = reinterpret_cast<const GpuGeom*>(sc.image + sc.off_geoms);
     }
+    __syncthreads();
     uint4* st = reinterpret_cast<uint4*>(smem + kp.lds_stack_off) + tid;
     uint4* spill = kp.spill + (blockIdx.x * BLOCK + (uint32_t)tid);
     const uint32_t spill_stride = kp.total_lanes;
-    const float4* qo = wf.q_o[wf.bounce & 1];
-    const float4* qd = wf.q_d[wf.bounce & 1];
+    const size_t seg0 = (size_t)g * wf.seg;
+    const float4* qo = wf.q_o[wf.bounce & 1] + seg0;
+    const float4* qd = wf.q_d[wf.bounce & 1] + seg0;
+    float4* hit = wf.hit + seg0;
 
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0};
     SlotCursor cur_chunk = {0, kChunk};
@@ -188,8 +211,8 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
     RayState r;
     r.htri = -1;
     int mode = kDead;
-    uint32_t slot = cur_chunk.take(true, &cn->fetched), depth = 0;
-    uint32_t nslot = cur_chunk.take(true, &cn->fetched);
+    uint32_t slot = cur_chunk.take(true, lcnt + 4), depth = 0;
+    uint32_t nslot = cur_chunk.take(true, lcnt + 4);
     float4 no4 = make_float4(0, 0, 0, 0), nd4 = make_float4(0, 0, 0, 0);
     auto start = [&](float4 o4, float4 d4) {
         r.o = xyz(o4);
@@ -218,16 +241,16 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
         const bool fin = mode == kReady;
         uint32_t cls = 4u;
         if (fin) {
-            wf.hit[slot] = make_float4(r.best, r.hbeta, r.hgamma, __int_as_float(r.htri));
+            hit[slot] = make_float4(r.best, r.hbeta, r.hgamma, __int_as_float(r.htri));
             cls = kClassTerminate;
             if (r.htri >= 0 && depth != kNoRay && (int32_t)depth < kp.max_depth) {
-                const GpuGeom& g = geoms[__float_as_uint(tris[3 * r.htri + 1].w)];
-                if (!is_emitter(g)) cls = material_class(g);
+                const GpuGeom& gm = geoms[__float_as_uint(tris[3 * r.htri + 1].w)];
+                if (!is_emitter(gm)) cls = material_class(gm);
             }
         }
 #pragma unroll
         for (uint32_t k = 0; k < 4; k++)
-            out[k].append(cls == k, slot, &cn->cls[k], wf.cls_list + (size_t)k * wf.capacity);
+            out[k].append(cls == k, slot, lcnt + k, wf.cls_list + (size_t)k * wf.slot_stride + seg0);
         // ---- finished lanes start their prefetched ray, prefetch another ------
         if (fin) {
             if (nslot < count) {
@@ -238,7 +261,7 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
             }
         }
         const bool want = fin && mode != kDead;
-        const uint32_t ns = cur_chunk.take(want, &cn->fetched);
+        const uint32_t ns = cur_chunk.take(want, lcnt + 4);
         if (want) {
             nslot = ns;
             if (nslot < count) { no4 = qo[nslot]; nd4 = qd[nslot]; }
@@ -246,32 +269,40 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
         if (!__ballot(mode != kDead)) break;
     }
 #pragma unroll
-    for (uint32_t k = 0; k < 4; k++) out[k].flush(&cn->cls[k], wf.cls_list + (size_t)k * wf.capacity);
+    for (uint32_t k = 0; k < 4; k++) out[k].flush(lcnt + k, wf.cls_list + (size_t)k * wf.slot_stride + seg0);
     flush_counters(c, kp.stats);
+    __syncthreads();
+    if (tid < 4) cn->cls[tid] = lcnt[tid];
 }
 
-// ---- shade: the class lists back to back (CUTracer.cu:105-175) -------------
-// Items are taken in the order [diffuse, phong, fresnel, terminate]; the i-th
-// continuing item writes its next ray to slot i of queue b+1 (no atomics), so
-// consecutive waves shade one material each.
-__global__ void __launch_bounds__(kShadeBlock) wf_shade(const KernelParams kp, const WfParams wf) {
-    WfCounters* cn = wf.cnt + wf.bounce;
-    WfCounters* nx = cn + 1;
+// ---- shade: each segment's class lists back to back (CUTracer.cu:105-175) ---
+// Items of segment g are taken in the order [diffuse, phong, fresnel,
+// terminate]; the i-th continuing item writes its next ray to slot i of the
+// segment's queue b+1 (no atomics), so consecutive waves shade one material.
+// `per` workgroups share a segment, each a contiguous share of its items.
+__global__ void __launch_bounds__(kShadeBlock) wf_shade(const KernelParams kp, const WfParams wf, uint32_t per) {
+    const uint32_t g = blockIdx.x / per, q = blockIdx.x - g * per;
+    if (g >= wf.nseg) return;
+    const WfCounters* cn = wf.cnt + (size_t)wf.bounce * wf.nseg + g;
+    WfCounters* nx = wf.cnt + (size_t)(wf.bounce + 1) * wf.nseg + g;
     const GpuScene& sc = kp.scene;
     const float4* tris = reinterpret_cast<const float4*>(sc.image + sc.off_tris);
     const GpuGeom* geoms = reinterpret_cast<const GpuGeom*>(sc.image + sc.off_geoms);
-    const float4* qo = wf.q_o[wf.bounce & 1];
-    const float4* qd = wf.q_d[wf.bounce & 1];
-    float4* qo2 = wf.q_o[(wf.bounce + 1) & 1];
-    float4* qd2 = wf.q_d[(wf.bounce + 1) & 1];
+    const size_t seg0 = (size_t)g * wf.seg;
+    const float4* qo = wf.q_o[wf.bounce & 1] + seg0;
+    const float4* qd = wf.q_d[wf.bounce & 1] + seg0;
+    const float4* hit = wf.hit + seg0;
+    float4* qo2 = wf.q_o[(wf.bounce + 1) & 1] + seg0;
+    float4* qd2 = wf.q_d[(wf.bounce + 1) & 1] + seg0;
     const uint32_t p1 = cn->cls[1], p2 = p1 + cn->cls[2], p3 = p2 + cn->cls[3], total = p3 + cn->cls[0];
-    if (blockIdx.x == 0 && threadIdx.x == 0) nx->queued = p3;
+    if (q == 0 && threadIdx.x == 0) nx->queued = p3;
+    const uint32_t lo = (uint32_t)(((uint64_t)total * q) / per), hi = (uint32_t)(((uint64_t)total * (q + 1)) / per);
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (uint32_t i = blockIdx.x * kShadeBlock + threadIdx.x; i < total; i += gridDim.x * kShadeBlock) {
+    for (uint32_t i = lo + threadIdx.x; i < hi; i += kShadeBlock) {
         const uint32_t k = i < p1 ? 1u : (i < p2 ? 2u : (i < p3 ? 3u : 0u));
         const uint32_t start = k == 1u ? 0u : (k == 2u ? p1 : (k == 3u ? p2 : p3));
-        const uint32_t slot = wf.cls_list[(size_t)k * wf.capacity + (i - start)];
-        const float4 o4 = qo[slot], d4 = qd[slot], h = wf.hit[slot];
+        const uint32_t slot = wf.cls_list[(size_t)k * wf.slot_stride + seg0 + (i - start)];
+        const float4 o4 = qo[slot], d4 = qd[slot], h = hit[slot];
         const uint32_t pid = __float_as_uint(o4.w);
         const uint32_t depth = __float_as_uint(d4.w);
         const int32_t htri = __float_as_int(h.w);
@@ -279,18 +310,18 @@ __global__ void __launch_bounds__(kShadeBlock) wf_shade(const KernelParams kp, c
             // miss -> 0; emitter -> color*Ka*ILLUM (:111-113); terminal query (:162-175)
             V3 L = v3(0, 0, 0);
             if (htri >= 0 && depth != kNoRay) {
-                const GpuGeom& g = geoms[__float_as_uint(tris[3 * htri + 1].w)];
-                if ((int32_t)depth >= kp.max_depth || is_emitter(g)) L = emitted(xyz(wf.pstate[pid]), g, kp.illum);
+                const GpuGeom& gm = geoms[__float_as_uint(tris[3 * htri + 1].w)];
+                if ((int32_t)depth >= kp.max_depth || is_emitter(gm)) L = emitted(xyz(wf.pstate[pid]), gm, kp.illum);
             }
             wf.radiance[pid] = make_float4(L.x, L.y, L.z, 0.0f);
         } else {
             c.shades++;
             const float4 ps = wf.pstate[pid];
             V3 color = xyz(ps);
-            const GpuGeom& g = geoms[__float_as_uint(tris[3 * htri + 1].w)];
+            const GpuGeom& gm = geoms[__float_as_uint(tris[3 * htri + 1].w)];
             uint32_t sd = __float_as_uint(ps.w);
             V3 o = xyz(o4), d = xyz(d4);
-            scatter(g, sc.normals, htri, h.y, h.z, h.x, kp.fresnel_kd, sd, color, o, d);
+            scatter(gm, sc.normals, htri, h.y, h.z, h.x, kp.fresnel_kd, sd, color, o, d);
             wf.pstate[pid] = pack(color, sd);
             qo2[i] = pack(o, pid);
             qd2[i] = pack(d, depth + 1u);
@@ -319,20 +350,29 @@ hipError_t launch_extend(const KernelParams& kp, const WfParams& wf, int grid, s
     return hipGetLastError();
 }
 
+bool wf_in_lds(uint32_t image_bytes) { return lds_bytes_in_lds(image_bytes, 4) + 32 <= kMaxLds; }
+
 }  // namespace
+
+int wavefront_segments(uint32_t image_bytes, int cus) {
+    return wf_in_lds(image_bytes) ? cus : cus * kGlobalBlocksPerCu;
+}
 
 hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams& wf_in, int cus, int max_bounces,
                             hipStream_t st, hipEvent_t ev0, hipEvent_t ev1, hipEvent_t ev2, float4* fb,
                             int* variant_out) {
     KernelParams kp = kp_in;
     const uint32_t img = kp.scene.image_bytes;
-    const bool in_lds = lds_bytes_in_lds(img, 4) <= kMaxLds;
+    const bool in_lds = wf_in_lds(img);
     kp.lds_stack_off = in_lds ? img : 0u;
     kp.total_lanes = (uint32_t)total_lanes_for(img, cus);
+    const uint32_t nseg = (uint32_t)wavefront_segments(img, cus);
+    const uint32_t per = in_lds ? 4u : 1u;                         // shade workgroups per segment
     hipError_t e = hipSuccess;
     if (ev0) hipEventRecord(ev0, st);
     for (uint32_t chunk = 0; chunk < kp.nchunks; chunk++) {
         WfParams wf = wf_in;
+        wf.nseg = nseg;
         wf.chunk_index = chunk;
         wf.s_begin = chunk * kp.chunk;
         wf.ns = (kp.spp - wf.s_begin) < kp.chunk ? (kp.spp - wf.s_begin) : kp.chunk;
@@ -340,9 +380,10 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams& wf_in, in
         for (uint32_t v0 = 0; v0 < kp.npix_local; v0 += nb_max) {
             wf.v0 = v0;
             wf.nb = (kp.npix_local - v0) < nb_max ? (kp.npix_local - v0) : nb_max;
-            e = hipMemsetAsync(wf.cnt, 0, sizeof(WfCounters) * (size_t)(max_bounces + 1), st);
-            if (e != hipSuccess) return e;
             const uint32_t n = wf.nb * wf.ns;
+            wf.seg = ((n + 63u) / 64u + nseg - 1) / nseg * 64u;      // whole 64-path groups per segment
+            e = hipMemsetAsync(wf.cnt, 0, sizeof(WfCounters) * (size_t)nseg * (size_t)(max_bounces + 1), st);
+            if (e != hipSuccess) return e;
             const uint32_t gen_grid = (n + kGenBlock - 1) / kGenBlock;
             hipLaunchKernelGGL(wf_generate, dim3(gen_grid < 16u * (uint32_t)cus ? gen_grid : 16u * (uint32_t)cus),
                                dim3(kGenBlock), 0, st, kp, wf);
@@ -350,12 +391,12 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams& wf_in, in
             for (int b = 0; b < max_bounces; b++) {
                 wf.bounce = b;
                 if (in_lds)
-                    e = launch_extend<true, 4, kLdsBlock>(kp, wf, cus, lds_bytes_in_lds(img, 4), st);
+                    e = launch_extend<true, 4, kLdsBlock>(kp, wf, (int)nseg, lds_bytes_in_lds(img, 4) + 32, st);
                 else
-                    e = launch_extend<false, 8, kGlobalBlock>(kp, wf, cus * kGlobalBlocksPerCu,
-                                                              (size_t)8 * kGlobalBlock * 16, st);
+                    e = launch_extend<false, 8, kGlobalBlock>(kp, wf, (int)nseg, (size_t)8 * kGlobalBlock * 16 + 32,
+                                                              st);
                 if (e != hipSuccess) return e;
-                hipLaunchKernelGGL(wf_shade, dim3(cus * 8), dim3(kShadeBlock), 0, st, kp, wf);
+                hipLaunchKernelGGL(wf_shade, dim3(nseg * per), dim3(kShadeBlock), 0, st, kp, wf, per);
                 if ((e = hipGetLastError()) != hipSuccess) return e;
             }
             hipLaunchKernelGGL(wf_accumulate, dim3((wf.nb + 255u) / 256u), dim3(256), 0, st, kp, wf);

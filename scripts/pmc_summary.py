@@ -12,13 +12,15 @@ import json
 import os
 import sys
 
+MATCH = os.environ.get("KERNEL_MATCH", "path_kernel")
+
 
 def read_counters(d):
     vals = {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                if "path_kernel" not in row.get("Kernel_Name", ""):
+                if MATCH not in row.get("Kernel_Name", ""):
                     continue
                 k = row["Counter_Name"]
                 vals.setdefault(k, {}).setdefault(row["Dispatch_Id"], 0.0)
@@ -43,7 +45,7 @@ def main(out):
     for f in glob.glob(os.path.join(out, "kt", "**", "*kernel_stats.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                if "path_kernel" in row["Name"]:
+                if MATCH in row["Name"]:
                     kstats = {"name": row["Name"], "calls": int(row["Calls"]), "avg_ns": float(row["AverageNs"])}
     d = {}
     rays = bench["rays_per_step"] if bench else None

@@ -11,8 +11,8 @@ OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 cd /tmp
-B="python3 $R/bench.py --no-cpu-baseline"
-timeout -k 10 300 python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/bench.jsonl 2> $OUT/bench.err
+B="python3 $R/bench.py --no-cpu-baseline $BENCH_ARGS"
+timeout -k 10 300 $B --steps 3 --warmup 1 > $OUT/bench.jsonl 2> $OUT/bench.err
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o run -- $B --steps 2 --warmup 1 > $OUT/kt.log 2>&1
 pass() {   # name counters...
   local n=$1; shift
