@@ -285,8 +285,8 @@ void prepare_workspace(mcpt_scene& s, mcpt::KernelParams& k) {
 mcpt::WfParams prepare_wavefront(mcpt_scene& s, const Plan& pl) {
     const size_t cap = pl.wf_capacity;
     const size_t bounces = (size_t(pl.kp.max_depth) + 2) * size_t(mcpt::wavefront_segments(s.gpu.image_bytes, s.cus));
-    // segments hold whole 64-path groups: up to nseg*64 slots beyond the paths
-    const size_t cap_slots = cap + size_t(mcpt::wavefront_segments(s.gpu.image_bytes, s.cus)) * 64;
+    // segments hold whole path groups (<= 2^14): up to nseg groups of slots beyond the paths
+    const size_t cap_slots = cap + size_t(mcpt::wavefront_segments(s.gpu.image_bytes, s.cus)) * 16384;
     const size_t f4 = cap_slots * 16;
     const size_t need = 4 * f4 + f4 + 4 * cap_slots * 4 + 2 * f4 + bounces * sizeof(mcpt::WfCounters) + 256;
     ensure_buf(s.ws.wf, s.ws.wf_bytes, need);

@@ -87,7 +87,8 @@ struct WfParams {
     uint32_t capacity;                   // paths per batch
     uint32_t slot_stride;                // queue / class-list entries per array (>= nseg * seg)
     uint32_t v0, nb, s_begin, ns, chunk_index;
-    uint32_t nseg, seg;                  // segments (= extend workgroups) and paths per segment
+    uint32_t nseg, seg;                  // segments (= extend workgroups) and slots per segment
+    uint32_t group_shift;                // paths are dealt to segments in groups of 2^group_shift
     int32_t bounce;
     int32_t refill_thresh;               // idle lanes before an extend wave refills
 };

@@ -4,8 +4,8 @@
 // Same paths, same arithmetic as the megakernel (render.hip), reorganised as
 // queues in HBM so that every kernel does one kind of work:
 //   generate    one primary ray per (pixel, sample) of the batch into ray
-//               queue 0, 64-path groups (an 8x8 tile) dealt to the segments
-//               round-robin
+//               queue 0, path groups (an 8x8 tile; 256 tiles for scenes in
+//               global memory) dealt to the segments round-robin
 //   extend b    closest hit of every ray in queue b: one persistent workgroup
 //               per queue segment, scene image in LDS (or global); waves
 //               reserve slots 64 at a time from an LDS counter, each lane
@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "mcpt_device.hpp"
 #include "render_launch.hpp"
@@ -56,23 +57,24 @@ __device__ __forceinline__ float4 pack(V3 v, uint32_t w) { return make_float4(v.
 __device__ __forceinline__ V3 xyz(float4 v) { return v3(v.x, v.y, v.z); }
 
 // ---- generate: primary rays of the batch (CUTracer.cu:186-211) -------------
-// Paths go to segments in groups of 64 (one 8x8 tile of one sample: a
-// coherent wave of primary rays), group j -> segment j % nseg, so every
-// segment holds tiles from all over the image and the workgroups finish
-// together.
+// Paths go to segments in groups of 2^group_shift (64 = one 8x8 tile of one
+// sample: a coherent wave of primary rays), group j -> segment j % nseg, so
+// every segment holds tiles from all over the image and the workgroups
+// finish together.
 __global__ void __launch_bounds__(kGenBlock) wf_generate(const KernelParams kp, const WfParams wf) {
     const uint32_t n = wf.nb * wf.ns;
-    const uint32_t ngroups = (n + 63u) / 64u;
+    const uint32_t gs = wf.group_shift, gm = (1u << gs) - 1u;
+    const uint32_t ngroups = (n + gm) >> gs;
     const V3 eye = v3(kp.eye[0], kp.eye[1], kp.eye[2]);
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0};
     for (uint32_t pid = blockIdx.x * kGenBlock + threadIdx.x; pid < n; pid += gridDim.x * kGenBlock) {
         const uint32_t s_local = pid / wf.nb;
         const uint32_t v = wf.v0 + (pid - s_local * wf.nb);
-        const uint32_t grp = pid >> 6, g = grp % wf.nseg;
-        const uint32_t slot = g * wf.seg + (grp / wf.nseg) * 64u + (pid & 63u);
-        if (grp < wf.nseg && (pid & 63u) == 0u) {   // first path of segment g: its queue length
-            uint32_t len = ((ngroups - g + wf.nseg - 1u) / wf.nseg) * 64u;
-            if ((ngroups - 1u) % wf.nseg == g) len -= ngroups * 64u - n;
+        const uint32_t grp = pid >> gs, g = grp % wf.nseg;
+        const uint32_t slot = g * wf.seg + ((grp / wf.nseg) << gs) + (pid & gm);
+        if (grp < wf.nseg && (pid & gm) == 0u) {    // first path of segment g: its queue length
+            uint32_t len = ((ngroups - g + wf.nseg - 1u) / wf.nseg) << gs;
+            if ((ngroups - 1u) % wf.nseg == g) len -= (ngroups << gs) - n;
             wf.cnt[g].queued = len;
         }
         int px, py;
@@ -352,6 +354,15 @@ hipError_t launch_extend(const KernelParams& kp, const WfParams& wf, int grid, s
 
 bool wf_in_lds(uint32_t image_bytes) { return lds_bytes_in_lds(image_bytes, 4) + 32 <= kMaxLds; }
 
+// global-memory scenes keep whole image regions together per segment (C4
+// sweep: 2^6 0.63, 2^8 0.47, 2^10 0.44, 2^12 0.62, contiguous 0.79 G rays/s);
+// MCPT_WF_GROUP_SHIFT overrides for experiments
+uint32_t wf_global_group_shift() {
+    const char* e = std::getenv("MCPT_WF_GROUP_SHIFT");
+    const int v = e ? std::atoi(e) : 14;
+    return (uint32_t)(v < 6 ? 6 : (v > 14 ? 14 : v));
+}
+
 }  // namespace
 
 int wavefront_segments(uint32_t image_bytes, int cus) {
@@ -381,7 +392,9 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams& wf_in, in
             wf.v0 = v0;
             wf.nb = (kp.npix_local - v0) < nb_max ? (kp.npix_local - v0) : nb_max;
             const uint32_t n = wf.nb * wf.ns;
-            wf.seg = ((n + 63u) / 64u + nseg - 1) / nseg * 64u;      // whole 64-path groups per segment
+            wf.group_shift = in_lds ? 6u : wf_global_group_shift();
+            // whole groups per segment
+            wf.seg = ((((n + (1u << wf.group_shift) - 1u) >> wf.group_shift) + nseg - 1) / nseg) << wf.group_shift;
             e = hipMemsetAsync(wf.cnt, 0, sizeof(WfCounters) * (size_t)nseg * (size_t)(max_bounces + 1), st);
             if (e != hipSuccess) return e;
             const uint32_t gen_grid = (n + kGenBlock - 1) / kGenBlock;
