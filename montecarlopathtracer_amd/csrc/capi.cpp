@@ -99,6 +99,7 @@ struct mcpt_scene {
     int device = -1;
     int cus = 0;
     std::vector<unsigned char> image;   // host copy of the device image
+    std::vector<uint32_t> tri_order;    // image triangle slot -> kd id
     mcpt::GpuScene gpu{};
     void* d_image = nullptr;
     void* d_normals = nullptr;
@@ -123,48 +124,145 @@ struct mcpt_scene {
 
 namespace {
 
+// Device node order: 128-B "treelet" clusters.  A cluster holds the sibling
+// pairs of the 3 levels below its root (<= 7 pairs = 112 B) and never
+// straddles a 128-B line, so one line serves 3 levels of a descent; clusters
+// are emitted breadth-first (the top of the tree comes first).  Slot 0 is
+// padding and slot 1 the root, so the root's own cluster fills line 0.
+// Triangles and leaf references are renumbered in the order the leaves
+// appear, so a leaf's triangles sit near its neighbours'.  Only addresses
+// change: traversal order, results and counters are those of the BFS tree.
+struct DeviceOrder {
+    std::vector<uint32_t> node_new;     // host node -> device node index
+    uint32_t n_slots = 0;               // device node indices in use (incl. padding)
+    std::vector<uint32_t> leaf_order;   // host leaf nodes in device order
+    std::vector<uint32_t> tri_order;    // device triangle slot -> kd id
+    std::vector<uint32_t> tri_new;      // kd id -> device triangle slot
+};
+
+DeviceOrder device_order(const mcpt::HostScene& hs, bool align_lines) {
+    const uint32_t nn = static_cast<uint32_t>(hs.nodes.size());
+    DeviceOrder d;
+    d.node_new.assign(nn, 0xFFFFFFFFu);
+    d.node_new[0] = 0;
+    uint32_t pairs = 0;                  // pair m occupies device nodes 2m+1, 2m+2 (slots 2m+2, 2m+3)
+    std::vector<uint32_t> queue{0}, list, frontier, next;
+    for (size_t qi = 0; qi < queue.size(); ++qi) {
+        list.clear();
+        frontier.assign(1, queue[qi]);
+        for (int lvl = 0; lvl < 3; ++lvl) {
+            next.clear();
+            for (uint32_t n : frontier)
+                if (hs.nodes[n].axis) {
+                    list.push_back(hs.nodes[n].left);
+                    next.push_back(hs.nodes[n].left);
+                    next.push_back(hs.nodes[n].left + 1);
+                }
+            frontier.swap(next);
+        }
+        for (uint32_t n : frontier)
+            if (hs.nodes[n].axis) queue.push_back(n);
+        if (list.empty()) continue;
+        const uint32_t used = (pairs + 1) % 8;                  // pairs already in the current line
+        if (align_lines && used && used + list.size() > 8) pairs += 8 - used;  // start a fresh line
+        for (uint32_t L : list) {
+            d.node_new[L] = 2 * pairs + 1;
+            d.node_new[L + 1] = 2 * pairs + 2;
+            ++pairs;
+        }
+    }
+    d.n_slots = 2 * pairs + 1;
+    // leaves in device order, triangles by first appearance
+    std::vector<uint32_t> by_dev(d.n_slots, 0xFFFFFFFFu);
+    for (uint32_t i = 0; i < nn; ++i) by_dev[d.node_new[i]] = i;
+    d.tri_new.assign(hs.kd_tris.size(), 0xFFFFFFFFu);
+    for (uint32_t dv = 0; dv < d.n_slots; ++dv) {
+        const uint32_t i = by_dev[dv];
+        if (i == 0xFFFFFFFFu || hs.nodes[i].axis) continue;
+        d.leaf_order.push_back(i);
+        for (uint32_t r = 0; r < hs.nodes[i].leaf_count; ++r) {
+            const uint32_t k = hs.leaf_ids[hs.nodes[i].leaf_begin + r];
+            if (d.tri_new[k] == 0xFFFFFFFFu) {
+                d.tri_new[k] = static_cast<uint32_t>(d.tri_order.size());
+                d.tri_order.push_back(k);
+            }
+        }
+    }
+    for (uint32_t k = 0; k < d.tri_new.size(); ++k)
+        if (d.tri_new[k] == 0xFFFFFFFFu) {
+            d.tri_new[k] = static_cast<uint32_t>(d.tri_order.size());
+            d.tri_order.push_back(k);
+        }
+    return d;
+}
+
 void build_image(mcpt_scene& s) {
     const mcpt::HostScene& hs = s.hs;
     const uint32_t nt = static_cast<uint32_t>(hs.kd_tris.size());
     const uint32_t nn = static_cast<uint32_t>(hs.nodes.size());
     const uint32_t nl = static_cast<uint32_t>(hs.leaf_ids.size());
     const uint32_t ng = static_cast<uint32_t>(hs.geoms.size());
+    for (uint32_t i = 0; i < nn; ++i)
+        if (hs.nodes[i].axis && (hs.nodes[i].left % 2u) != 1u)
+            throw mcpt::Error{MCPT_E_INVALID, "KD sibling pair not at an odd index"};
     auto al16 = [](size_t x) { return (x + 15u) & ~size_t(15); };
+    auto al128 = [](size_t x) { return (x + 127u) & ~size_t(127); };
+    // scenes that fit in LDS keep the packed order (no cache lines there, every
+    // byte counts); larger ones get line-aligned clusters
+    DeviceOrder ord = device_order(hs, false);
+    auto image_size = [&](const DeviceOrder& o, size_t& on, size_t& ol, size_t& og) {
+        on = al128(size_t(nt) * 48);
+        // node slot j = device node j-1 (slot 0 = padding): pairs are aligned 16-B records
+        ol = al16(on + size_t(o.n_slots + 1) * 8);
+        og = al16(ol + size_t(nl) * 4);
+        return al16(og + size_t(ng) * 64);
+    };
+    size_t off_nodes, off_leafs, off_geoms;
+    size_t total = image_size(ord, off_nodes, off_leafs, off_geoms);
+    if (mcpt::lds_bytes_in_lds(static_cast<uint32_t>(std::min<size_t>(total, 0xFFFFFFF0u)), 4) + 32 > mcpt::kMaxLds) {
+        ord = device_order(hs, true);
+        total = image_size(ord, off_nodes, off_leafs, off_geoms);
+    }
     const size_t off_tris = 0;
-    const size_t off_nodes = al16(off_tris + size_t(nt) * 48);
-    // nodes are stored one slot late (slot 0 = padding): BFS puts every sibling
-    // pair at odd indices [2k+1, 2k+2], so each pair becomes one aligned 16-B record
-    const size_t off_leafs = al16(off_nodes + size_t(nn + 1) * 8);
-    const size_t off_geoms = al16(off_leafs + size_t(nl) * 4);
-    const size_t total = al16(off_geoms + size_t(ng) * 64);
     if (total > 0xFFFFFFF0u) throw mcpt::Error{MCPT_E_UNSUPPORTED, "scene image exceeds 4 GiB"};
-    if (nn >= (1u << 30) || nl >= (1u << 30)) throw mcpt::Error{MCPT_E_UNSUPPORTED, "KD tree too large"};
+    if (ord.n_slots >= (1u << 30) || nl >= (1u << 30)) throw mcpt::Error{MCPT_E_UNSUPPORTED, "KD tree too large"};
     s.image.assign(total, 0);
+    s.tri_order = ord.tri_order;
     unsigned char* img = s.image.data();
-    for (uint32_t k = 0; k < nt; ++k) {
+    for (uint32_t slot = 0; slot < nt; ++slot) {
+        const uint32_t k = ord.tri_order[slot];
         const float* v = &hs.kd_verts[9 * size_t(k)];
         float rec[12] = {v[0], v[1], v[2], 0.0f,
                          v[0] - v[3], v[1] - v[4], v[2] - v[5], 0.0f,
                          v[0] - v[6], v[1] - v[7], v[2] - v[8], 0.0f};
         std::memcpy(&rec[3], &hs.kd_prio[k], 4);
         std::memcpy(&rec[7], &hs.kd_geom[k], 4);
-        std::memcpy(img + off_tris + size_t(k) * 48, rec, 48);
+        std::memcpy(img + off_tris + size_t(slot) * 48, rec, 48);
+    }
+    // leaf references, leaves in device order
+    std::vector<uint32_t> leaf_begin_new(nn, 0);
+    {
+        uint32_t* refs = reinterpret_cast<uint32_t*>(img + off_leafs);
+        uint32_t at = 0;
+        for (uint32_t i : ord.leaf_order) {
+            leaf_begin_new[i] = at;
+            for (uint32_t r = 0; r < hs.nodes[i].leaf_count; ++r)
+                refs[at++] = ord.tri_new[hs.leaf_ids[hs.nodes[i].leaf_begin + r]];
+        }
     }
     for (uint32_t i = 0; i < nn; ++i) {
         const mcpt::KdNode& n = hs.nodes[i];
         uint32_t w[2];
         if (n.axis) {
-            w[0] = ((n.axis - 1u) << 30) | n.left;
+            w[0] = ((n.axis - 1u) << 30) | ord.node_new[n.left];
             std::memcpy(&w[1], &n.split, 4);
         } else {
-            w[0] = (3u << 30) | n.leaf_begin;
+            w[0] = (3u << 30) | leaf_begin_new[i];
             w[1] = n.leaf_count;
         }
-        if (n.axis && (n.left % 2u) != 1u) throw mcpt::Error{MCPT_E_INVALID, "KD sibling pair not at an odd index"};
-        std::memcpy(img + off_nodes + size_t(i + 1) * 8, w, 8);
+        std::memcpy(img + off_nodes + size_t(ord.node_new[i] + 1) * 8, w, 8);
         if (i == 0) { s.gpu.root_w[0] = w[0]; s.gpu.root_w[1] = w[1]; }
     }
-    if (nl) std::memcpy(img + off_leafs, hs.leaf_ids.data(), size_t(nl) * 4);
     for (uint32_t g = 0; g < ng; ++g) {
         const mcpt::Geometry& ge = hs.geoms[g];
         mcpt::GpuGeom gg{};
@@ -560,9 +658,10 @@ static int scene_create_impl(const mcpt_model* m, mcpt_scene** out, bool device)
             HIP_TRY(hipMemcpy(s->d_image, s->image.data(), s->image.size(), hipMemcpyHostToDevice));
             const size_t nt = s->hs.kd_tris.size();
             std::vector<float> nrm(nt * 12, 0.0f);
-            for (size_t k = 0; k < nt; ++k)
+            for (size_t k = 0; k < nt; ++k)          // image triangle order
                 for (int j = 0; j < 3; ++j)
-                    for (int c = 0; c < 3; ++c) nrm[12 * k + 4 * j + c] = s->hs.kd_normals[9 * k + 3 * j + c];
+                    for (int c = 0; c < 3; ++c)
+                        nrm[12 * k + 4 * j + c] = s->hs.kd_normals[9 * size_t(s->tri_order[k]) + 3 * j + c];
             HIP_TRY(hipMalloc(&s->d_normals, nrm.size() * 4));
             HIP_TRY(hipMemcpy(s->d_normals, nrm.data(), nrm.size() * 4, hipMemcpyHostToDevice));
             s->gpu.image = static_cast<const unsigned char*>(s->d_image);

@@ -71,6 +71,11 @@ def main(out):
                 d["frac_wave_cycles_" + k[3:].lower()] = g(k) / wc
     if g("SQ_LDS_BANK_CONFLICT") and g("SQ_INSTS_LDS"):
         d["lds_bank_conflict_cycles_per_lds_instr"] = g("SQ_LDS_BANK_CONFLICT") / g("SQ_INSTS_LDS")
+    if g("TCC_HIT") is not None and g("TCC_MISS") is not None:
+        d["l2_hit_rate"] = g("TCC_HIT") / max(g("TCC_HIT") + g("TCC_MISS"), 1.0)
+        d["l2_requests_GB_x128B"] = (g("TCC_HIT") + g("TCC_MISS")) * 128 / 1e9
+    if g("TCP_TOTAL_CACHE_ACCESSES") and g("TCP_TCC_READ_REQ") is not None:
+        d["l1_miss_to_l2_frac"] = g("TCP_TCC_READ_REQ") / g("TCP_TOTAL_CACHE_ACCESSES")
     if g("GRBM_GUI_ACTIVE") and kstats:
         d["effective_clock_GHz"] = g("GRBM_GUI_ACTIVE") / 8 / kstats["avg_ns"]
     print(json.dumps({"kernel": kstats, "per_launch_counters": per, "derived": d, "bench_line": bench}, indent=1))
