@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define MCPT_ABI_VERSION 2
+#define MCPT_ABI_VERSION 3
 
 enum {
     MCPT_OK = 0,
@@ -85,7 +85,20 @@ typedef struct {
     int32_t packed;             /* 1: write owned tiles packed (tile-major) instead of row-major */
     int32_t pipeline;           /* MCPT_PIPELINE_*: megakernel (default) or wavefront; same image */
     uint32_t wf_batch;          /* wavefront: max paths in flight per batch, 0 = 1<<24 */
+    int32_t mode;               /* MCPT_MODE_*: path semantics (default CVMCTracer)       */
+    int32_t reserved_;          /* 0 */
 } mcpt_render_params;
+
+enum {
+    /* CVMCTracer/CUDA/CUTracer.cu:98-218: 7 scatters + terminal query, ILLUM,
+       +-1 px jitter, linear running mean, horizontal fov_deg */
+    MCPT_MODE_CVMCTRACER = 0,
+    /* MCRT/QuinEngine/Shader/rtx.hlsl:304-405: Russian roulette from bounce
+       max_depth, stop at 3*max_depth, no ILLUM, no Fresnel Kd, +-0.5 px jitter,
+       near-plane origin, gamma-2.2 running mean, t_best 10000, vertical
+       fov_deg, seed = the 32-bit frame seed (GraphicsRTX.cpp:163-193) */
+    MCPT_MODE_QUINENGINE = 1
+};
 
 enum {
     MCPT_PIPELINE_MEGAKERNEL = 0,   /* one persistent kernel per render (render.hip) */
@@ -118,6 +131,9 @@ int mcpt_init(const int32_t* devices, int32_t n_devices);
 int mcpt_device_count(int32_t* out);
 /* fill defaults = the CVMCTracer constants for scene 1 (CUTracer.cu:347-360) */
 void mcpt_render_params_default(mcpt_render_params* p);
+/* QuinEngine viewer defaults (GraphicsRTX.cpp:163-193, rtx.hlsl:373-404):
+ * mode QE, 800x600, 1 spp per frame, depth 5, fovY 45, eye (0,5,17)        */
+void mcpt_render_params_quinengine(mcpt_render_params* p);
 
 /* ---- host model (ObjModel) ---------------------------------------------- */
 /* In-memory ObjModel, laid out like ObjReader.hpp:57-63 (element 0 of every

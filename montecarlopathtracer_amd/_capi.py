@@ -21,7 +21,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MCPT_LIB_PATH") or os.path.join(_HERE, "lib", "libmcpt.so")
 
 MCPT_OK = 0
-ABI_VERSION = 2
+ABI_VERSION = 3
+MODE_CVMCTRACER = 0
+MODE_QUINENGINE = 1
 PIPELINE_MEGAKERNEL = 0
 PIPELINE_WAVEFRONT = 1
 ERRORS = {-1: "INVALID", -2: "IO", -3: "PARSE", -4: "DEVICE", -5: "NOMEM", -6: "UNSUPPORTED"}
@@ -51,7 +53,7 @@ class RenderParamsC(C.Structure):
         ("eye", C.c_float * 3), ("dir", C.c_float * 3), ("up", C.c_float * 3),
         ("seed", C.c_uint64), ("prev_count", C.c_uint32), ("fresnel_kd", C.c_int32),
         ("tile", C.c_int32), ("shard_count", C.c_int32), ("shard_index", C.c_int32), ("packed", C.c_int32),
-        ("pipeline", C.c_int32), ("wf_batch", C.c_uint32),
+        ("pipeline", C.c_int32), ("wf_batch", C.c_uint32), ("mode", C.c_int32), ("reserved_", C.c_int32),
     ]
 
 
@@ -85,6 +87,7 @@ _SIGS = {
     "mcpt_init": (C.c_int, [C.POINTER(C.c_int32), C.c_int32]),
     "mcpt_device_count": (C.c_int, [C.POINTER(C.c_int32)]),
     "mcpt_render_params_default": (None, [C.POINTER(RenderParamsC)]),
+    "mcpt_render_params_quinengine": (None, [C.POINTER(RenderParamsC)]),
     "mcpt_model_create": (C.c_int, [C.POINTER(ModelDesc), C.POINTER(_vp)]),
     "mcpt_model_read_obj": (C.c_int, [C.c_char_p, C.POINTER(_vp)]),
     "mcpt_model_free": (None, [_vp]),

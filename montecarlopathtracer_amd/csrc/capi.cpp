@@ -345,7 +345,22 @@ Plan make_plan(const mcpt_scene& s, const mcpt_render_params* p) {
     k.fwd[0] = d.x; k.fwd[1] = d.y; k.fwd[2] = d.z;
     k.up[0] = u.x; k.up[1] = u.y; k.up[2] = u.z;
     k.right[0] = r.x; k.right[1] = r.y; k.right[2] = r.z;
-    k.key = tea16(static_cast<uint32_t>(p->seed), static_cast<uint32_t>(p->seed >> 32));
+    if (p->mode != MCPT_MODE_CVMCTRACER && p->mode != MCPT_MODE_QUINENGINE)
+        throw mcpt::Error{MCPT_E_INVALID, "unknown mode"};
+    k.mode = p->mode;
+    k.best_init = FLT_MAX;
+    if (p->mode == MCPT_MODE_QUINENGINE) {
+        // rtx.hlsl:380 seeds TEA-16 with the 32-bit frame seed itself; t_best 10000 (:88);
+        // camera GraphicsRTX.cpp:173-184 (PerspectiveFovRH: fov_deg is the vertical FOV)
+        k.key = static_cast<uint32_t>(p->seed);
+        k.best_init = 10000.0f;
+        const float a = p->fov_deg * 3.14159265359f / 360;
+        const float ys = static_cast<float>(1.0 / std::tan(static_cast<double>(a)));
+        k.proj22 = ys;
+        k.proj11 = ys / (static_cast<float>(p->width) / static_cast<float>(p->height));
+    } else {
+        k.key = tea16(static_cast<uint32_t>(p->seed), static_cast<uint32_t>(p->seed >> 32));
+    }
     {
         const char* e = std::getenv("MCPT_READY_THRESH");
         const int th = e ? std::atoi(e) : 32;
@@ -382,7 +397,8 @@ void prepare_workspace(mcpt_scene& s, mcpt::KernelParams& k) {
 // path state and radiance, per-bounce counters -- carved from one buffer
 mcpt::WfParams prepare_wavefront(mcpt_scene& s, const Plan& pl) {
     const size_t cap = pl.wf_capacity;
-    const size_t bounces = (size_t(pl.kp.max_depth) + 2) * size_t(mcpt::wavefront_segments(s.gpu.image_bytes, s.cus));
+    const size_t queries = pl.kp.mode == MCPT_MODE_QUINENGINE ? 3 * size_t(pl.kp.max_depth) + 1 : size_t(pl.kp.max_depth) + 1;
+    const size_t bounces = (queries + 1) * size_t(mcpt::wavefront_segments(s.gpu.image_bytes, s.cus));
     // segments hold whole path groups (<= 2^14): up to nseg groups of slots beyond the paths
     const size_t cap_slots = cap + size_t(mcpt::wavefront_segments(s.gpu.image_bytes, s.cus)) * 16384;
     const size_t f4 = cap_slots * 16;
@@ -432,7 +448,8 @@ void render_async(mcpt_scene& s, const mcpt_render_params* p, float* d_fb, hipSt
     if (pl.pipeline == MCPT_PIPELINE_WAVEFRONT) {
         if (d_unit_counters) throw mcpt::Error{MCPT_E_UNSUPPORTED, "unit counters need the megakernel pipeline"};
         const mcpt::WfParams wf = prepare_wavefront(s, pl);
-        HIP_TRY(mcpt::launch_wavefront(pl.kp, wf, s.cus, pl.kp.max_depth + 1, st, t.e[0], t.e[1], t.e[2],
+        const int queries = pl.kp.mode == MCPT_MODE_QUINENGINE ? 3 * pl.kp.max_depth + 1 : pl.kp.max_depth + 1;
+        HIP_TRY(mcpt::launch_wavefront(pl.kp, wf, s.cus, queries, st, t.e[0], t.e[1], t.e[2],
                                        reinterpret_cast<float4*>(d_fb), &s.last_variant));
     } else {
         HIP_TRY(mcpt::launch_render(pl.kp, s.cus, st, t.e[0], t.e[1], t.e[2], reinterpret_cast<float4*>(d_fb),
@@ -504,6 +521,19 @@ int mcpt_device_count(int32_t* out) {
         *out = c;
         return MCPT_OK;
     });
+}
+
+void mcpt_render_params_quinengine(mcpt_render_params* p) {
+    if (!p) return;
+    mcpt_render_params_default(p);
+    p->mode = MCPT_MODE_QUINENGINE;
+    p->width = 800; p->height = 600;                 // window size of the QE viewer
+    p->spp = 1;                                       // one sample per pixel per frame (rtx.hlsl:373-404)
+    p->max_depth = 5;                                 // sampleMC(..., 5) (rtx.hlsl:400)
+    p->illum = 1.0f;                                  // no ILLUM factor
+    p->fov_deg = 45.0f;                               // D3DX_PI / 4, vertical (GraphicsRTX.cpp:181)
+    p->fresnel_kd = 0;                                // rtx.hlsl:345 (commented out)
+    p->seed = 0;                                      // frame seed: the caller's mt19937(1234) draw
 }
 
 void mcpt_render_params_default(mcpt_render_params* p) {

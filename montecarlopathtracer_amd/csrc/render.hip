@@ -33,7 +33,7 @@ using namespace trace;
 
 namespace {
 
-template <bool IN_LDS, int S, int BLOCK, bool DBG>
+template <bool IN_LDS, int S, int BLOCK, bool DBG, bool QE>
 __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = (int)threadIdx.x;
@@ -81,13 +81,17 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
     // start sample s of the current unit: primary ray, then its root interval
     auto start_path = [&]() {
         const uint32_t pix = (uint32_t)py * (uint32_t)kp.width + (uint32_t)px;
-        primary_ray(kp, pix, px, py, s, sd, r.d);
-        r.o = eye;
+        if constexpr (QE) {
+            primary_ray_qe(kp, pix, px, py, s, sd, r.o, r.d);
+        } else {
+            primary_ray(kp, pix, px, py, s, sd, r.d);
+            r.o = eye;
+        }
         color = v3(1, 1, 1);
         depth = 0;
         c.paths++;
         c.rays++;
-        mode = begin_ray(r, sc) ? kTrav : kReady;
+        mode = begin_ray(r, sc, kp.best_init) ? kTrav : kReady;
     };
 
 #ifdef MCPT_PHASE_TIMING
@@ -148,7 +152,25 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
         if (mode == kReady) {
             bool done = false;
             V3 L = v3(0, 0, 0);
-            if (depth < kp.max_depth) {
+            if constexpr (QE) {
+                // rtx.hlsl:309-370: miss or bounce >= 3*depth ends the path; roulette
+                // from bounce `depth` on; emitters return color*Ka (no ILLUM)
+                if (r.htri < 0 || depth >= 3 * kp.max_depth || (depth >= kp.max_depth && !qe_roulette(sd, color))) {
+                    done = true;
+                } else {
+                    const GpuGeom& g = geoms[__float_as_uint(tris[3 * r.htri + 1].w)];
+                    if (is_emitter(g)) {
+                        L = emitted(color, g, 1.0f);
+                        done = true;
+                    } else {
+                        c.shades++;
+                        scatter(g, sc.normals, r.htri, r.hbeta, r.hgamma, r.best, 0, sd, color, r.o, r.d);
+                        depth++;
+                        c.rays++;
+                        mode = begin_ray(r, sc, kp.best_init) ? kTrav : kReady;
+                    }
+                }
+            } else if (depth < kp.max_depth) {
                 if (r.htri < 0) {
                     done = true;
                 } else {
@@ -162,7 +184,7 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
                         scatter(g, sc.normals, r.htri, r.hbeta, r.hgamma, r.best, kp.fresnel_kd, sd, color, r.o, r.d);
                         depth++;
                         c.rays++;
-                        mode = begin_ray(r, sc) ? kTrav : kReady;
+                        mode = begin_ray(r, sc, kp.best_init) ? kTrav : kReady;
                     }
                 }
             } else {
@@ -219,7 +241,11 @@ __global__ void __launch_bounds__(256) reduce_kernel(const KernelParams kp, floa
     const V3 mean = vdiv(sum, (float)kp.spp);
     const size_t idx = kp.packed ? (size_t)v : (size_t)y * (size_t)kp.width + (size_t)x;
     float4 out;
-    if (kp.prev_count == 0) {
+    if (kp.mode == kModeQE) {   // gamma-space running mean (rtx.hlsl:401-402)
+        const float4 pv = kp.prev_count ? fb[idx] : make_float4(0, 0, 0, 0);
+        out = make_float4(qe_blend(pv.x, mean.x, kp.prev_count), qe_blend(pv.y, mean.y, kp.prev_count),
+                          qe_blend(pv.z, mean.z, kp.prev_count), 0.0f);
+    } else if (kp.prev_count == 0) {
         out = make_float4(mean.x, mean.y, mean.z, 0.0f);
     } else {
         const float4 pv = fb[idx];
@@ -231,7 +257,9 @@ __global__ void __launch_bounds__(256) reduce_kernel(const KernelParams kp, floa
 
 template <bool IN_LDS, int S, int BLOCK>
 hipError_t launch_path(const KernelParams& kp, int grid, size_t lds, hipStream_t st) {
-    auto kern = kp.unit_counters ? path_kernel<IN_LDS, S, BLOCK, true> : path_kernel<IN_LDS, S, BLOCK, false>;
+    const bool qe = kp.mode == kModeQE;
+    auto kern = kp.unit_counters ? (qe ? path_kernel<IN_LDS, S, BLOCK, true, true> : path_kernel<IN_LDS, S, BLOCK, true, false>)
+                                 : (qe ? path_kernel<IN_LDS, S, BLOCK, false, true> : path_kernel<IN_LDS, S, BLOCK, false, false>);
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;

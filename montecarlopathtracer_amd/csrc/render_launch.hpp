@@ -52,6 +52,9 @@ struct KernelParams {
     float illum, tan_half_fov;
     int32_t fresnel_kd;
     uint32_t prev_count;
+    int32_t mode;                        // 0 CVMCTracer, 1 QuinEngine (rtx.hlsl:304-405)
+    float proj11, proj22;                // QE projection scales (PerspectiveFovRH)
+    float best_init;                     // closest-hit start: FLT_MAX, QE 10000 (rtx.hlsl:88)
     float eye[3], fwd[3], up[3], right[3];
     uint32_t key;                        // TEA-16 key of the 64-bit seed
     float4* partial;                     // [nchunks][npix_local]

@@ -43,13 +43,13 @@ struct RayState {
 };
 
 // root interval (oracle: isect_kd_ordered prologue); returns false on a miss
-__device__ __forceinline__ bool begin_ray(RayState& r, const GpuScene& sc) {
+__device__ __forceinline__ bool begin_ray(RayState& r, const GpuScene& sc, float best_init) {
     r.ix = 1.0f / r.d.x;
     r.iy = 1.0f / r.d.y;
     r.iz = 1.0f / r.d.z;
     r.htri = -1;
     r.hbeta = r.hgamma = 0.0f;
-    r.best = kFltMax;
+    r.best = best_init;
     r.bprio = 0xFFFFFFFFu;
     r.nw0 = sc.root_w[0];
     r.nw1 = sc.root_w[1];
@@ -281,6 +281,47 @@ __device__ __forceinline__ void flush_counters(const Counters& c, unsigned long 
         for (int i = 0; i < 8; i++)
             if (vals[i]) atomicAdd(stats + i, (unsigned long long)vals[i]);
     }
+}
+
+
+// ---- QuinEngine semantics (rtx.hlsl:304-405) ----------------------------------
+constexpr int32_t kModeQE = 1;
+constexpr float kQeGamma = 2.2f;
+constexpr float kQeInvGamma = 0.454545454545f;   // 1 / 2.2 as float
+// primary ray: TEA-16(pixel, frame seed) + two warm-up draws, +-0.5 px jitter,
+// origin on the near plane z = -1 of the view, view -> world by the basis
+__device__ __forceinline__ void primary_ray_qe(const KernelParams& kp, uint32_t pix, int px, int py, uint32_t s,
+                                               uint32_t& sd, V3& o, V3& dir) {
+    sd = tea16(pix, kp.key + kp.spp_offset + s);
+    (void)rng_next(sd);
+    (void)rng_next(sd);
+    const float bx = (float)(uint32_t)px + (rng_next(sd) - 0.5f);
+    const float by = (float)(uint32_t)py + (rng_next(sd) - 0.5f);
+    const float vx = (2.0f * bx / (float)(uint32_t)kp.width - 1.0f) / kp.proj11;
+    const float vy = (1.0f - 2.0f * by / (float)(uint32_t)kp.height) / kp.proj22;
+    const float vz = -1.0f;
+    V3 w;
+    w.x = kp.right[0] * vx + kp.up[0] * vy - kp.fwd[0] * vz;
+    w.y = kp.right[1] * vx + kp.up[1] * vy - kp.fwd[1] * vz;
+    w.z = kp.right[2] * vx + kp.up[2] * vy - kp.fwd[2] * vz;
+    o = v3(w.x + kp.eye[0], w.y + kp.eye[1], w.z + kp.eye[2]);
+    normalize_cu(w);
+    dir = w;
+}
+// Russian roulette from bounce `depth` on (rtx.hlsl:314-325); false = path dies
+__device__ __forceinline__ bool qe_roulette(uint32_t& sd, V3& color) {
+    const float illum = fmaxf(fmaxf(color.x, color.y), color.z);
+    if (illum > rng_next(sd)) {
+        color = vdiv(color, illum);
+        return true;
+    }
+    return false;
+}
+// gamma-space running mean (rtx.hlsl:401-402)
+__device__ __forceinline__ float qe_blend(float old, float c, uint32_t prev) {
+    if (prev == 0) return pow_f(c, kQeInvGamma);
+    const float pc = (float)prev, pc1 = (float)(prev + 1u);
+    return pow_f((pow_f(old, kQeGamma) * pc + c) / pc1, kQeInvGamma);
 }
 
 }  // namespace trace

@@ -80,16 +80,20 @@ __global__ void __launch_bounds__(kGenBlock) wf_generate(const KernelParams kp, 
         int px, py;
         V3 d = v3(0, 0, 0);
         uint32_t depth = kNoRay;
+        V3 o = eye;
         if (unit_pixel(kp, v, px, py)) {
             uint32_t sd;
             const uint32_t pix = (uint32_t)py * (uint32_t)kp.width + (uint32_t)px;
-            primary_ray(kp, pix, px, py, wf.s_begin + s_local, sd, d);
+            if (kp.mode == kModeQE)
+                primary_ray_qe(kp, pix, px, py, wf.s_begin + s_local, sd, o, d);
+            else
+                primary_ray(kp, pix, px, py, wf.s_begin + s_local, sd, d);
             wf.pstate[pid] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(sd));
             c.paths++;
             c.rays++;
             depth = 0;
         }
-        wf.q_o[0][slot] = pack(eye, pid);
+        wf.q_o[0][slot] = pack(o, pid);
         wf.q_d[0][slot] = pack(d, depth);
     }
     flush_counters(c, kp.stats);
@@ -224,7 +228,7 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
             r.htri = -1;
             mode = kReady;
         } else {
-            mode = begin_ray(r, sc) ? kTrav : kReady;
+            mode = begin_ray(r, sc, kp.best_init) ? kTrav : kReady;
         }
     };
     if (slot < count) start(qo[slot], qd[slot]);
@@ -245,7 +249,10 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
         if (fin) {
             hit[slot] = make_float4(r.best, r.hbeta, r.hgamma, __int_as_float(r.htri));
             cls = kClassTerminate;
-            if (r.htri >= 0 && depth != kNoRay && (int32_t)depth < kp.max_depth) {
+            // CV: scatter while depth < max_depth (CUTracer.cu:103-160); QE: while
+            // bounce < 3*depth (rtx.hlsl:312), roulette is drawn in shade
+            const int32_t lim = kp.mode == kModeQE ? 3 * kp.max_depth : kp.max_depth;
+            if (r.htri >= 0 && depth != kNoRay && (int32_t)depth < lim) {
                 const GpuGeom& gm = geoms[__float_as_uint(tris[3 * r.htri + 1].w)];
                 if (!is_emitter(gm)) cls = material_class(gm);
             }
@@ -308,26 +315,44 @@ __global__ void __launch_bounds__(kShadeBlock) wf_shade(const KernelParams kp, c
         const uint32_t pid = __float_as_uint(o4.w);
         const uint32_t depth = __float_as_uint(d4.w);
         const int32_t htri = __float_as_int(h.w);
+        const bool qe = kp.mode == kModeQE;
         if (k == kClassTerminate) {
-            // miss -> 0; emitter -> color*Ka*ILLUM (:111-113); terminal query (:162-175)
+            // CV: miss -> 0; emitter -> color*Ka*ILLUM (:111-113); terminal query (:162-175)
+            // QE: miss / bounce >= 3*depth -> 0; roulette, then emitter -> color*Ka (rtx.hlsl:312-331)
             V3 L = v3(0, 0, 0);
             if (htri >= 0 && depth != kNoRay) {
                 const GpuGeom& gm = geoms[__float_as_uint(tris[3 * htri + 1].w)];
-                if ((int32_t)depth >= kp.max_depth || is_emitter(gm)) L = emitted(xyz(wf.pstate[pid]), gm, kp.illum);
+                if (qe) {
+                    if ((int32_t)depth < 3 * kp.max_depth) {
+                        const float4 ps = wf.pstate[pid];
+                        V3 color = xyz(ps);
+                        uint32_t sd = __float_as_uint(ps.w);
+                        if ((int32_t)depth < kp.max_depth || qe_roulette(sd, color)) L = emitted(color, gm, 1.0f);
+                    }
+                } else if ((int32_t)depth >= kp.max_depth || is_emitter(gm)) {
+                    L = emitted(xyz(wf.pstate[pid]), gm, kp.illum);
+                }
             }
             wf.radiance[pid] = make_float4(L.x, L.y, L.z, 0.0f);
         } else {
-            c.shades++;
             const float4 ps = wf.pstate[pid];
             V3 color = xyz(ps);
-            const GpuGeom& gm = geoms[__float_as_uint(tris[3 * htri + 1].w)];
             uint32_t sd = __float_as_uint(ps.w);
-            V3 o = xyz(o4), d = xyz(d4);
-            scatter(gm, sc.normals, htri, h.y, h.z, h.x, kp.fresnel_kd, sd, color, o, d);
-            wf.pstate[pid] = pack(color, sd);
-            qo2[i] = pack(o, pid);
-            qd2[i] = pack(d, depth + 1u);
-            c.rays++;
+            if (qe && (int32_t)depth >= kp.max_depth && !qe_roulette(sd, color)) {
+                // killed by the roulette: zero radiance, an empty slot in queue b+1
+                wf.radiance[pid] = make_float4(0, 0, 0, 0);
+                qo2[i] = pack(v3(0, 0, 0), pid);
+                qd2[i] = pack(v3(0, 0, 0), kNoRay);
+            } else {
+                c.shades++;
+                const GpuGeom& gm = geoms[__float_as_uint(tris[3 * htri + 1].w)];
+                V3 o = xyz(o4), d = xyz(d4);
+                scatter(gm, sc.normals, htri, h.y, h.z, h.x, qe ? 0 : kp.fresnel_kd, sd, color, o, d);
+                wf.pstate[pid] = pack(color, sd);
+                qo2[i] = pack(o, pid);
+                qd2[i] = pack(d, depth + 1u);
+                c.rays++;
+            }
         }
     }
     flush_counters(c, kp.stats);

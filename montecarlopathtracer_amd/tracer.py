@@ -144,6 +144,7 @@ class ObjModel:
 
 
 PIPELINES = {"megakernel": _capi.PIPELINE_MEGAKERNEL, "wavefront": _capi.PIPELINE_WAVEFRONT}
+MODES = {"cvmctracer": _capi.MODE_CVMCTRACER, "quinengine": _capi.MODE_QUINENGINE}
 
 
 @dataclass
@@ -169,12 +170,23 @@ class RenderParams:
     packed: bool = False
     pipeline: str = "megakernel"      # or "wavefront" (C5): identical image, different kernels
     wf_batch: int = 0                 # wavefront paths in flight per batch, 0 = 1<<24
+    mode: str = "cvmctracer"          # or "quinengine": rtx.hlsl path semantics (see for_quinengine)
 
     @staticmethod
     def for_scene(scene_id: int, **kw) -> "RenderParams":
         """Camera of RenderScene(sceneID) (CUTracer.cu:347-374)."""
         eye = (0.0, 5.0, 17.0) if scene_id == 1 else (0.0, 5.0, 23.0)
         return RenderParams(eye=eye, **kw)
+
+    @staticmethod
+    def for_quinengine(**kw) -> "RenderParams":
+        """QuinEngine viewer frame (GraphicsRTX.cpp:163-193, rtx.hlsl:373-404): 1 spp,
+        depth 5 with Russian roulette, vertical FOV 45, no ILLUM / Fresnel Kd,
+        gamma-2.2 running mean; `seed` is the 32-bit frame seed."""
+        base = dict(width=800, height=600, spp=1, spp_chunk=1, max_depth=5, illum=1.0, fov_deg=45.0,
+                    fresnel_kd=False, seed=0, mode="quinengine")
+        base.update(kw)
+        return RenderParams(**base)
 
     def to_c(self) -> RenderParamsC:
         p = RenderParamsC()
@@ -193,6 +205,9 @@ class RenderParams:
             raise ValueError(f"pipeline must be one of {sorted(PIPELINES)}")
         p.pipeline = PIPELINES[self.pipeline]
         p.wf_batch = int(self.wf_batch)
+        if self.mode not in MODES:
+            raise ValueError(f"mode must be one of {sorted(MODES)}")
+        p.mode = MODES[self.mode]
         return p
 
     def output_pixels(self) -> int:

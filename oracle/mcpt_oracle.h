@@ -18,6 +18,9 @@
  *   - samplers                  CV/CUDA/Utils.hpp:46-137
  *   - path loop                 CV/CUDA/CUTracer.cu:98-177
  *   - primary ray + accumulate  CV/CUDA/CUTracer.cu:179-218, camera :347-374
+ *   - QuinEngine mode (mode 1)  QE/Shader/rtx.hlsl:304-405 (Russian roulette, no ILLUM,
+ *                               no Fresnel Kd, +-0.5 px jitter, gamma accumulation,
+ *                               t_best 10000), camera QE/RTX/GraphicsRTX.cpp:173-184
  *
  * Where the reference is not reproducible, the build's own specification is
  * used (DESIGN.md "Determinism spec"):
@@ -63,6 +66,8 @@ typedef struct {
     uint32_t prev_count;            /* running-mean count (CUTracer.cu:215-217)  */
     int32_t fresnel_kd;             /* 1: color *= Kd on Fresnel (CUTracer.cu:131-133);
                                        0: no tint (rtx.hlsl:345, the published renders) */
+    int32_t mode;                   /* 0: CVMCTracer semantics; 1: QuinEngine (rtx.hlsl:304-405) */
+    float proj11, proj22;           /* QE: PerspectiveFovRH scales (orc_qe_proj)  */
 } orc_params;
 
 typedef struct {
@@ -110,6 +115,8 @@ void orc_sample_hemi(const float* n, const float* u, float* out);
 void orc_sample_phong(const float* n, const float* in, uint32_t Ns, const float* u, float* out);
 void orc_sample_fresnel(const float* n, const float* in, float Tr, float Ni, const float* u, float* out);
 float orc_tan_half_fov(float fov_deg);
+/* QE camera (GraphicsRTX.cpp:181-182): D3DXMatrixPerspectiveFovRH(fovY, W/H) diagonal */
+void orc_qe_proj(float fovy_deg, int32_t width, int32_t height, float* p11, float* p22);
 void orc_camera_basis(const float* eye, const float* dir, const float* up,
                       float* fwd_out, float* up_out, float* right_out);
 

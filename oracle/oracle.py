@@ -16,6 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "build", "libmcpt_oracle.so")
 
 BRUTE, KD_REF, KD_ORDERED = 0, 1, 2
+MODE_CV, MODE_QE = 0, 1
 
 
 class Params(C.Structure):
@@ -27,6 +28,7 @@ class Params(C.Structure):
         ("eye", C.c_float * 3), ("fwd", C.c_float * 3), ("up", C.c_float * 3), ("right", C.c_float * 3),
         ("seed", C.c_uint64), ("traversal", C.c_int32), ("threads", C.c_int32),
         ("prev_count", C.c_uint32), ("fresnel_kd", C.c_int32),
+        ("mode", C.c_int32), ("proj11", C.c_float), ("proj22", C.c_float),
     ]
 
 
@@ -90,6 +92,8 @@ def lib():
         L.orc_sample_fresnel.argtypes = [f32p, f32p, C.c_float, C.c_float, f32p, f32p]
         L.orc_tan_half_fov.restype = C.c_float
         L.orc_tan_half_fov.argtypes = [C.c_float]
+        L.orc_qe_proj.restype = None
+        L.orc_qe_proj.argtypes = [C.c_float, C.c_int32, C.c_int32, f32p, f32p]
         L.orc_camera_basis.argtypes = [f32p] * 6
         L.orc_intersect_batch.argtypes = [vp, C.c_int, C.c_int64, f32p, f32p, i32p, i32p, f32p, C.POINTER(Counters)]
         L.orc_render.restype = C.c_int
@@ -196,7 +200,7 @@ class RenderParams:
 
     def __init__(self, width=64, height=64, spp=4, spp_offset=0, spp_chunk=0, max_depth=7, illum=10.0,
                  fov=60.0, scene_id=1, eye=None, direction=(0, 0, -1), up=(0, 1, 0), seed=0x4D435054,
-                 traversal=KD_ORDERED, threads=1, region=None, prev_count=0, fresnel_kd=1):
+                 traversal=KD_ORDERED, threads=1, region=None, prev_count=0, fresnel_kd=1, mode=MODE_CV):
         self.width, self.height, self.spp, self.spp_offset, self.spp_chunk = width, height, spp, spp_offset, spp_chunk
         self.max_depth, self.illum, self.fov, self.seed = max_depth, illum, fov, seed
         if eye is None:
@@ -204,6 +208,7 @@ class RenderParams:
         self.eye, self.direction, self.up = eye, direction, up
         self.traversal, self.threads, self.prev_count, self.fresnel_kd = traversal, threads, prev_count, fresnel_kd
         self.region = region or (0, 0, width, height)
+        self.mode = mode
 
     def to_c(self):
         P = Params()
@@ -217,4 +222,9 @@ class RenderParams:
         P.fwd[:] = f.tolist(); P.up[:] = u.tolist(); P.right[:] = r.tolist()
         P.seed = self.seed
         P.traversal, P.threads, P.prev_count, P.fresnel_kd = self.traversal, self.threads, self.prev_count, self.fresnel_kd
+        P.mode = self.mode
+        if self.mode == MODE_QE:
+            p11, p22 = C.c_float(), C.c_float()
+            lib().orc_qe_proj(C.c_float(self.fov), self.width, self.height, C.byref(p11), C.byref(p22))
+            P.proj11, P.proj22 = p11.value, p22.value
         return P

@@ -267,6 +267,13 @@ float orc_tan_half_fov(float fov_deg) {
     float a = fov_deg * PW_PI / 360;
     return (float)tan((double)a);
 }
+/* yScale = cot(fovY/2), xScale = yScale / aspect (D3DXMatrixPerspectiveFovRH) */
+void orc_qe_proj(float fovy_deg, int32_t width, int32_t height, float* p11, float* p22) {
+    float a = fovy_deg * PW_PI / 360;
+    float ys = (float)(1.0 / tan((double)a));
+    *p22 = ys;
+    *p11 = ys / ((float)width / (float)height);
+}
 
 /* ======================== closest-hit queries ============================= */
 float orc_det3(const float* m) {   /* Math.hpp:169-175 */
@@ -287,6 +294,7 @@ typedef struct {
     const orc_scene* s;
     const orc_v3 (*kv)[3];   /* vertices by kd id */
     int traversal;
+    float best_init;         /* FLT_MAX (CUTracer.cu:46); 10000 in QE mode (rtx.hlsl:88) */
     orc_counters c;
 } qctx;
 
@@ -327,7 +335,7 @@ static hit_t isect_brute(qctx* q, orc_v3 o, orc_v3 d) {
     hit_t h;
     memset(&h, 0, sizeof h);
     h.tri = -1; h.geom = -1;
-    float tmin = FLT_MAX;
+    float tmin = q->best_init;
     for (int g = 0; g < s->ngeoms; g++) {
         uint32_t off = s->geoms[g].start;
         for (uint32_t i = 0; i < s->geoms[g].count; i++) {
@@ -367,7 +375,7 @@ static hit_t isect_kd_ref(qctx* q, orc_v3 o, orc_v3 d) {
     hit_t h;
     memset(&h, 0, sizeof h);
     h.tri = -1; h.geom = -1;
-    float tmin = FLT_MAX;
+    float tmin = q->best_init;
     uint32_t bprio = 0xFFFFFFFFu;
     uint32_t stack[96];
     int top = 0;
@@ -399,7 +407,7 @@ static hit_t isect_kd_ordered(qctx* q, orc_v3 o, orc_v3 d) {
     hit_t h;
     memset(&h, 0, sizeof h);
     h.tri = -1; h.geom = -1;
-    float best = FLT_MAX;
+    float best = q->best_init;
     uint32_t bprio = 0xFFFFFFFFu;
     float oo[3] = {o.x, o.y, o.z}, dd[3] = {d.x, d.y, d.z};
     float inv[3] = {1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
@@ -485,6 +493,7 @@ void orc_intersect_batch(const orc_scene* s, int traversal, int64_t n,
     memset(&q, 0, sizeof q);
     q.s = s;
     q.traversal = traversal;
+    q.best_init = FLT_MAX;
     orc_v3(*kv)[3] = malloc(sizeof(orc_v3[3]) * (size_t)(s->nkd ? s->nkd : 1));
     for (int k = 0; k < s->nkd; k++)
         for (int j = 0; j < 3; j++) kv[k][j] = s->model.verts[s->model.tris[s->kd_tris[k]].v[j]];
@@ -559,6 +568,86 @@ static orc_v3 sample_mc(qctx* q, usrc* u, orc_v3 pos, orc_v3 dir, int max_depth,
     return color;
 }
 
+
+/* ===================== QuinEngine path (rtx.hlsl:304-371) ================= */
+#define QE_T_BEST 10000.0f
+static orc_v3 sample_mc_qe(qctx* q, usrc* u, orc_v3 pos, orc_v3 dir, int depth_lim) {
+    const orc_scene* s = q->s;
+    orc_v3 color = v3(1, 1, 1);
+    uint32_t bounce = 0;
+    q->c.paths++;
+    hit_t hit = intersect(q, pos, dir);
+    while (hit.geom != -1) {
+        if (bounce >= (uint32_t)depth_lim * 3u) return v3(0, 0, 0);
+        if (bounce >= (uint32_t)depth_lim) {                  /* Russian roulette, :314-325 */
+            float illum = fmaxf(fmaxf(color.x, color.y), color.z);
+            if (illum > next_u(u)) color = vdiv(color, illum);
+            else return v3(0, 0, 0);
+        }
+        const orc_geom* g = &s->geoms[hit.geom];
+        if (g->Ka.x > 0 || g->Ka.y > 0 || g->Ka.z > 0) {     /* :327-331, no ILLUM */
+            color.x *= g->Ka.x * 1.0f; color.y *= g->Ka.y * 1.0f; color.z *= g->Ka.z * 1.0f;
+            return color;
+        }
+        q->c.shades++;
+        const orc_tri* t = &s->model.tris[s->kd_tris[hit.tri]];
+        orc_v3 n1 = s->model.normals[t->n[0]];
+        orc_v3 n2 = s->model.normals[t->n[1]];
+        orc_v3 n3 = s->model.normals[t->n[2]];
+        orc_v3 normal = vadd(vadd(vscale(n1, 1.0f - hit.beta - hit.gamma), vscale(n2, hit.beta)), vscale(n3, hit.gamma));
+        normalize_cu(&normal);
+        if (g->Tr > 0) {                                      /* :341-345, no Kd tint */
+            dir = sample_fresnel(u, normal, dir, g->Tr, g->Ni);
+        } else if (g->Ns > 1) {
+            dir = sample_phong(u, normal, dir, (uint32_t)g->Ns);
+            color.x *= g->Ks.x; color.y *= g->Ks.y; color.z *= g->Ks.z;
+        } else {
+            color.x *= g->Kd.x; color.y *= g->Kd.y; color.z *= g->Kd.z;
+            if (dot3(dir, normal) > 0) {
+                orc_v3 h = sample_hemi(u, normal);
+                dir = v3(-h.x, -h.y, -h.z);
+            } else {
+                dir = sample_hemi(u, normal);
+            }
+        }
+        pos = vadd(hit.hp, vscale(dir, 0.01f));
+        hit = intersect(q, pos, dir);
+        ++bounce;
+    }
+    return v3(0, 0, 0);
+}
+
+/* QE primary ray (rtx.hlsl:380-397): TEA-16(pixel, frame seed), two warm-up
+ * draws, +-0.5 px jitter, near-plane origin, view->world by the camera basis */
+static void qe_primary(const orc_params* p, uint32_t pix, int x, int y, uint32_t sample, usrc* u,
+                       orc_v3* o, orc_v3* d) {
+    u->sd = orc_tea16(pix, (uint32_t)p->seed + p->spp_offset + sample);
+    u->inj = NULL; u->k = 0;
+    next_u(u);
+    next_u(u);
+    float bx = (float)(uint32_t)x + (next_u(u) - 0.5f);
+    float by = (float)(uint32_t)y + (next_u(u) - 0.5f);
+    float vx = (2.0f * bx / (float)(uint32_t)p->width - 1.0f) / p->proj11;
+    float vy = (1.0f - 2.0f * by / (float)(uint32_t)p->height) / p->proj22;
+    float vz = -1.0f;
+    orc_v3 w;
+    w.x = p->right[0] * vx + p->up[0] * vy - p->fwd[0] * vz;
+    w.y = p->right[1] * vx + p->up[1] * vy - p->fwd[1] * vz;
+    w.z = p->right[2] * vx + p->up[2] * vy - p->fwd[2] * vz;
+    *o = v3(w.x + p->eye[0], w.y + p->eye[1], w.z + p->eye[2]);
+    normalize_cu(&w);
+    *d = w;
+}
+
+/* gamma-space running mean (rtx.hlsl:401-402) with the deterministic pow */
+#define QE_GAMMA 2.2f
+#define QE_INV_GAMMA 0.454545454545f
+static float qe_blend(float old, float c, uint32_t prev) {
+    if (prev == 0) return orc_powf(c, QE_INV_GAMMA);
+    float pc = (float)prev, pc1 = (float)(prev + 1u);
+    return orc_powf((orc_powf(old, QE_GAMMA) * pc + c) / pc1, QE_INV_GAMMA);
+}
+
 /* ========================= render (CUTracer.cu:179-218) =================== */
 typedef struct {
     const orc_scene* s;
@@ -584,6 +673,13 @@ static void render_pixel(qctx* q, const orc_params* p, uint32_t key, int x, int 
         orc_v3 part = v3(0, 0, 0);
         uint32_t c1 = c0 + chunk < p->spp ? c0 + chunk : p->spp;
         for (uint32_t i = c0; i < c1; i++) {
+            if (p->mode == 1) {
+                usrc u;
+                orc_v3 o, d;
+                qe_primary(p, pix, x, y, i, &u, &o, &d);
+                part = vadd(part, sample_mc_qe(q, &u, o, d, p->max_depth));
+                continue;
+            }
             usrc u = {orc_rng_init(pix, key, p->spp_offset + i), NULL, 0};
             float biasx = (float)(uint32_t)x + (next_u(&u) * 2.0f - 1.0f);
             float biasy = (float)(uint32_t)y + (next_u(&u) * 2.0f - 1.0f);
@@ -602,7 +698,11 @@ static void render_pixel(qctx* q, const orc_params* p, uint32_t key, int x, int 
         sum = vadd(sum, part);
     }
     orc_v3 mean = vdiv(sum, (float)p->spp);
-    if (p->prev_count == 0) {
+    if (p->mode == 1) {
+        px[0] = qe_blend(px[0], mean.x, p->prev_count);
+        px[1] = qe_blend(px[1], mean.y, p->prev_count);
+        px[2] = qe_blend(px[2], mean.z, p->prev_count);
+    } else if (p->prev_count == 0) {
         px[0] = mean.x; px[1] = mean.y; px[2] = mean.z;
     } else {
         float pc = (float)p->prev_count, pc1 = (float)(p->prev_count + 1);
@@ -620,6 +720,7 @@ static void* render_worker(void* arg) {
     q.s = j->s;
     q.kv = j->kv;
     q.traversal = p->traversal;
+    q.best_init = p->mode == 1 ? QE_T_BEST : FLT_MAX;
     uint32_t key = orc_seed_key(p->seed);
     for (;;) {
         pthread_mutex_lock(&j->mu);

@@ -29,14 +29,23 @@ def test_library_exports_every_declared_symbol(mcpt):
 
 def test_abi_version_and_defaults(mcpt):
     from montecarlopathtracer_amd._capi import RenderParamsC, lib
-    assert lib().mcpt_abi_version() == 2
+    assert lib().mcpt_abi_version() == 3
     p = RenderParamsC()
     lib().mcpt_render_params_default(C.byref(p))
     # CV/stdafx.h:41-46, CUTracer.cu:189,212,349-351
     assert (p.width, p.height, p.spp, p.max_depth) == (800, 600, 100, 7)
     assert p.illum == 10.0 and p.fov_deg == 60.0
     assert list(p.eye) == [0, 5, 17] and list(p.dir) == [0, 0, -1] and list(p.up) == [0, 1, 0]
-    assert p.fresnel_kd == 1 and p.tile == 8
+    assert p.fresnel_kd == 1 and p.tile == 8 and p.mode == 0 and p.pipeline == 0
+    q = RenderParamsC()
+    lib().mcpt_render_params_quinengine(C.byref(q))
+    # QE/RTX/GraphicsRTX.cpp:173-193, QE/Shader/rtx.hlsl:400
+    assert (q.mode, q.spp, q.max_depth, q.fresnel_kd) == (1, 1, 5, 0)
+    assert q.fov_deg == 45.0 and list(q.eye) == [0, 5, 17] and q.illum == 1.0
+    # the Python mirror agrees with the C defaults
+    r = mcpt.RenderParams.for_quinengine().to_c()
+    for f in ("mode", "spp", "max_depth", "fresnel_kd", "fov_deg", "illum", "width", "height"):
+        assert getattr(r, f) == getattr(q, f), f
 
 
 def test_host_scene_errors(mcpt):

@@ -133,3 +133,52 @@ def test_wavefront_batches_equal_megakernel(mcpt, batch):
         assert np.array_equal(mk, wf)
         for k in ("rays", "paths", "inner_visits", "leaf_visits", "leaf_refs", "tri_tests", "shades"):
             assert smk[k] == swf[k], (k, smk[k], swf[k])
+
+
+QE_CASES = [
+    # scene, W, H, spp, chunk, depth, seed
+    ("scene01", 64, 48, 4, 2, 5, 1234),
+    ("scene01", 40, 30, 3, 0, 2, 0xDEADBEEF),
+    ("scene02", 48, 36, 2, 2, 5, 77),
+    ("cornell_bunny70k", 40, 32, 2, 1, 5, 5),
+]
+
+
+def _qe_params(mcpt, W, H, spp, chunk, depth, seed, **kw):
+    return mcpt.RenderParams.for_quinengine(width=W, height=H, spp=spp, spp_chunk=chunk, max_depth=depth,
+                                            seed=seed, **kw)
+
+
+@pytest.mark.parametrize("pipeline", ["megakernel", "wavefront"])
+@pytest.mark.parametrize("case", QE_CASES, ids=[f"qe-{c[0]}-{c[1]}x{c[2]}-d{c[5]}" for c in QE_CASES])
+def test_quinengine_mode_matches_oracle(mcpt, oracle_mod, case, pipeline):
+    """rtx.hlsl semantics (roulette, 3x depth cap, no ILLUM, gamma accumulation, QE camera)."""
+    sc, W, H, spp, chunk, depth, seed = case
+    path = mcpt.scene_path(sc)
+    o = oracle_mod.Scene(path)
+    ref, rc = o.render(oracle_mod.RenderParams(width=W, height=H, spp=spp, spp_chunk=chunk, max_depth=depth,
+                                               seed=seed, illum=1.0, fov=45.0, fresnel_kd=0, threads=8,
+                                               mode=oracle_mod.MODE_QE))
+    scene = mcpt.Scene(mcpt.ObjModel(path))
+    img, st = scene.render(_qe_params(mcpt, W, H, spp, chunk, depth, seed, pipeline=pipeline))
+    assert np.array_equal(img, ref), f"max abs diff {np.abs(img - ref).max()}"
+    for k in ("rays", "paths", "inner_visits", "leaf_visits", "leaf_refs", "tri_tests", "shades"):
+        assert st[k] == rc[k], (k, st[k], rc[k])
+    assert st["rays"] > st["paths"]
+
+
+@pytest.mark.parametrize("pipeline", ["megakernel", "wavefront"])
+def test_quinengine_progressive_frames_match_oracle(mcpt, oracle_mod, pipeline):
+    """Viewer loop: one spp per frame, new frame seed, prevCount = frame (rtx.hlsl:401-402)."""
+    path = mcpt.scene_path("scene01")
+    o = oracle_mod.Scene(path)
+    scene = mcpt.Scene(mcpt.ObjModel(path))
+    W, H = 32, 24
+    img = np.zeros((H, W, 3), np.float32)
+    ref = np.zeros((H, W, 3), np.float32)
+    for k, seed in enumerate([11, 2026, 3, 99999]):
+        scene.render(_qe_params(mcpt, W, H, 1, 1, 5, seed, prev_count=k, pipeline=pipeline), img)
+        ref, _ = o.render(oracle_mod.RenderParams(width=W, height=H, spp=1, spp_chunk=1, max_depth=5, seed=seed,
+                                                  illum=1.0, fov=45.0, fresnel_kd=0, threads=8, prev_count=k,
+                                                  mode=oracle_mod.MODE_QE), ref)
+        assert np.array_equal(img, ref), k

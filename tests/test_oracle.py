@@ -179,3 +179,20 @@ def test_statistical_pin_against_reference_render(scenes, oracle_mod):
     cur, _ = scenes["scene01"].render(oracle_mod.RenderParams(width=800, height=600, spp=16, illum=10.0, fresnel_kd=1,
                                                               traversal=oracle_mod.KD_ORDERED, threads=th))
     assert np.abs(blocks(cur) - blocks(ref))[unsat].mean() > 0.03
+
+
+def test_quinengine_mode_brute_equals_kd_and_is_gamma_encoded(oracle_mod, mcpt):
+    """QE mode (rtx.hlsl:304-405): same closest hits under brute force and the
+    ordered KD walk; roulette lengthens paths past `depth`; output is the
+    gamma-2.2 encoded running mean, so the emitter's Ka .78 reads .78^(1/2.2)."""
+    s = oracle_mod.Scene(mcpt.scene_path("scene01"))
+    kw = dict(width=40, height=30, spp=4, max_depth=5, illum=1.0, fov=45.0, fresnel_kd=0, threads=8,
+              mode=oracle_mod.MODE_QE, seed=1234)
+    a, ca = s.render(oracle_mod.RenderParams(traversal=oracle_mod.BRUTE, **kw))
+    b, cb = s.render(oracle_mod.RenderParams(traversal=oracle_mod.KD_ORDERED, **kw))
+    assert np.array_equal(a, b) and ca["rays"] == cb["rays"] and ca["shades"] == cb["shades"]
+    assert cb["rays"] / cb["paths"] > 3.0
+    assert abs(float(b.max()) - 0.78 ** (1 / 2.2)) < 2e-3
+    # depth 0: roulette from the first hit; with max_depth 1 paths are capped at 3 bounces
+    c, cc = s.render(oracle_mod.RenderParams(traversal=oracle_mod.KD_ORDERED, **dict(kw, max_depth=1)))
+    assert cc["rays"] <= 4 * cc["paths"]
