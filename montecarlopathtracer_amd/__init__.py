@@ -8,6 +8,7 @@ include/mcpt.h.  See DESIGN.md and INTEGRATION.md.
 Importing this package loads lib/libmcpt.so; there is no CPU fallback.
 """
 from ._capi import McptError, lib  # noqa: F401  (loads libmcpt.so, raises if missing)
+from .imageio import read_pfm, read_png, write_pfm, write_png
 from .scenes import scene_path
 from .tracer import (ILLUM, IMG_HEIGHT, IMG_WIDTH, NUM_KERNELS, NUM_SAMPLES_PER_KERNEL, CreateGeometry,
                      DestroyGeometry, Initialize, ObjModel, RenderParams, RenderScene, Scene, Tracer, encode_8bit)
@@ -16,4 +17,4 @@ lib()
 
 __all__ = ["McptError", "ObjModel", "RenderParams", "Scene", "Tracer", "Initialize", "CreateGeometry",
            "DestroyGeometry", "RenderScene", "encode_8bit", "scene_path", "IMG_WIDTH", "IMG_HEIGHT",
-           "NUM_KERNELS", "NUM_SAMPLES_PER_KERNEL", "ILLUM"]
+           "NUM_KERNELS", "NUM_SAMPLES_PER_KERNEL", "ILLUM", "write_png", "read_png", "write_pfm", "read_pfm"]

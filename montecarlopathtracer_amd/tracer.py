@@ -368,6 +368,4 @@ def RenderScene(sceneID: int, hostcolor: np.ndarray, **kw) -> int:
     return _default.render_scene(sceneID, hostcolor, **kw)
 
 
-def encode_8bit(hostcolor: np.ndarray) -> np.ndarray:
-    """8-bit RGB as main.cpp:19-29 writes it: value*255 saturated, no gamma."""
-    return np.clip(hostcolor * 255.0, 0, 255).astype(np.uint8)
+from .imageio import encode_8bit  # noqa: E402,F401  (main.cpp:19-29 encode; kept here for the API)

@@ -1,20 +1,28 @@
-"""Compile tests/cpp/pw_tracer_dropin.cpp against include/ and libmcpt.so (test infrastructure)."""
+"""Compile the C++ adapter test programs in tests/cpp/ against include/ (test infrastructure).
+
+pw_tracer_dropin  include/mcpt_pw_tracer.hpp: the CVMCTracer main.cpp call sequence
+qe_viewer         include/mcpt_qe_viewer.hpp: the QuinEngine OnUpdate frame loop
+image_io          include/mcpt_image_io.hpp: the main.cpp:19-29 encode, PNG and PFM
+"""
 import os
 import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
-OUT = os.path.join(HERE, "_build", "pw_tracer_dropin")
+LINKS_MCPT = {"pw_tracer_dropin": True, "qe_viewer": True, "image_io": False}
 
 
-def build():
-    os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    libdir = os.path.join(ROOT, "montecarlopathtracer_amd", "lib")
-    subprocess.run(["g++", "-std=c++17", "-O1", "-I" + os.path.join(ROOT, "include"),
-                    os.path.join(HERE, "pw_tracer_dropin.cpp"), "-L" + libdir, "-lmcpt",
-                    "-Wl,-rpath," + libdir, "-Wl,--allow-shlib-undefined", "-o", OUT], check=True)
-    return OUT
+def build(name: str = "pw_tracer_dropin") -> str:
+    out = os.path.join(HERE, "_build", name)
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    cmd = ["g++", "-std=c++17", "-O1", "-Wall", "-I" + os.path.join(ROOT, "include"), os.path.join(HERE, name + ".cpp")]
+    if LINKS_MCPT[name]:
+        libdir = os.path.join(ROOT, "montecarlopathtracer_amd", "lib")
+        cmd += ["-L" + libdir, "-lmcpt", "-Wl,-rpath," + libdir, "-Wl,--allow-shlib-undefined"]
+    subprocess.run(cmd + ["-o", out], check=True)
+    return out
 
 
 if __name__ == "__main__":
-    print(build())
+    for n in LINKS_MCPT:
+        print(build(n))

@@ -84,6 +84,7 @@ def test_pw_tracer_adapter_compiles_and_links(mcpt):
     sys.path.insert(0, os.path.join(ROOT, "tests", "cpp"))
     import build_dropin
     assert os.path.exists(build_dropin.build())
+    assert os.path.exists(build_dropin.build("qe_viewer"))      # include/mcpt_qe_viewer.hpp
 
 
 def test_struct_layouts_match_header(mcpt, tmp_path):

@@ -182,3 +182,29 @@ def test_quinengine_progressive_frames_match_oracle(mcpt, oracle_mod, pipeline):
                                                   illum=1.0, fov=45.0, fresnel_kd=0, threads=8, prev_count=k,
                                                   mode=oracle_mod.MODE_QE), ref)
         assert np.array_equal(img, ref), k
+
+
+def test_qe_viewer_adapter_frames(mcpt, tmp_path):
+    """include/mcpt_qe_viewer.hpp (Graphics::OnUpdate stand-in): mt19937(1234) frame
+    seeds, prevCount = frame, the saved PNG = the 8-bit encode of the screen."""
+    import os
+    import subprocess
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "cpp"))
+    import build_dropin
+    exe = build_dropin.build("qe_viewer")
+    W, H, F = 64, 48, 4
+    scr, png = str(tmp_path / "screen.bin"), str(tmp_path / "temp.png")
+    r = subprocess.run([exe, mcpt.scene_path("scene01"), str(W), str(H), str(F), scr, png],
+                       capture_output=True, text=True)
+    assert r.returncode == 0 and f"ok {F}" in r.stdout, r.stdout + r.stderr
+    seeds = [int(l.split()[1]) for l in r.stdout.splitlines() if l.startswith("seed")]
+    # std::mt19937(1234) + uniform_int_distribution<unsigned> over the full range: raw outputs
+    assert seeds[:2] == [822569775, 2137449171]
+    got = np.fromfile(scr, np.float32).reshape(H, W, 3)
+    scene = mcpt.Scene(mcpt.ObjModel(mcpt.scene_path("scene01")))
+    img = np.zeros((H, W, 3), np.float32)
+    for k, sd in enumerate(seeds):
+        scene.render(mcpt.RenderParams.for_quinengine(width=W, height=H, seed=sd, prev_count=k), img)
+    assert np.array_equal(got, img)
+    assert np.array_equal(mcpt.read_png(png), mcpt.encode_8bit(img))
