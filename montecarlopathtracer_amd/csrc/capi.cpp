@@ -479,8 +479,17 @@ void read_stats(mcpt_scene& s, mcpt_render_stats* out) {
         HIP_TRY(hipMemcpy(st, static_cast<char*>(s.ws.small) + 64, sizeof st, hipMemcpyDeviceToHost));
         HIP_TRY(hipMemset(static_cast<char*>(s.ws.small) + 64, 0, sizeof st));
         if (st[8] | st[9] | st[10] | st[11])   // diagnostic builds (-DMCPT_PHASE_TIMING) only
-            std::fprintf(stderr, "mcpt phase cycles (sum over waves): units %llu trav %llu shade %llu burst_iters %llu\n",
-                         st[8], st[9], st[10], st[11]);
+            std::fprintf(stderr, "mcpt phase cycles (sum over waves): units %llu trav %llu shade %llu burst_iters %llu "
+                         "scatter %llu\n", st[8], st[9], st[10], st[11], st[12]);
+#ifdef MCPT_PHASE_TIMING
+        {
+            unsigned long long lu[6];
+            mcpt::read_lane_use(lu);
+            std::fprintf(stderr, "mcpt lane use: descent %.3f (%llu wave-iters) triangle %.3f (%llu) burst %.3f (%llu)\n",
+                         lu[0] ? double(lu[1]) / (64.0 * lu[0]) : 0.0, lu[0], lu[2] ? double(lu[3]) / (64.0 * lu[2]) : 0.0,
+                         lu[2], lu[4] ? double(lu[5]) / (64.0 * lu[4]) : 0.0, lu[4]);
+        }
+#endif
         r.rays = st[0]; r.paths = st[1]; r.inner_visits = st[2]; r.leaf_visits = st[3];
         r.leaf_refs = st[4]; r.tri_tests = st[5]; r.shades = st[6]; r.stack_spills = st[7];
     }

@@ -68,18 +68,22 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
 
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0};
     Counters c0 = c;   // DBG builds only
+#ifdef MCPT_PHASE_TIMING
+    LaneUse lu = {0, 0, 0, 0, 0, 0};
+#endif
     int mode = kNeed;
     uint32_t s = 0, s_end = 0, unit_id = 0;
     int px = 0, py = 0, depth = 0;
     uint32_t sd = 1;
     V3 part = v3(0, 0, 0), color = v3(1, 1, 1);
+    float4 nf1 = make_float4(0, 0, 0, 0), nf2 = nf1, nf3 = nf1;   // prefetched shading normals
     RayState r;
     r.o = eye;
     r.d = v3(0, 0, -1);
     r.htri = -1;
 
-    // start sample s of the current unit: primary ray, then its root interval
-    auto start_path = [&]() {
+    // sample s of the current unit: its primary ray (the caller then starts it)
+    auto new_path = [&]() {
         const uint32_t pix = (uint32_t)py * (uint32_t)kp.width + (uint32_t)px;
         if constexpr (QE) {
             primary_ray_qe(kp, pix, px, py, s, sd, r.o, r.d);
@@ -90,12 +94,15 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
         color = v3(1, 1, 1);
         depth = 0;
         c.paths++;
+    };
+    // next query of this lane: count it, root interval (one inlined copy per phase)
+    auto start_ray = [&]() {
         c.rays++;
         mode = begin_ray(r, sc, kp.best_init) ? kTrav : kReady;
     };
 
 #ifdef MCPT_PHASE_TIMING
-    unsigned long long tm_units = 0, tm_trav = 0, tm_shade = 0, tm_iters = 0, tm_t0;
+    unsigned long long tm_units = 0, tm_trav = 0, tm_shade = 0, tm_iters = 0, tm_scatter = 0, tm_t0;
 #define MCPT_STAMP(acc) do { unsigned long long t1_ = __builtin_amdgcn_s_memtime(); acc += t1_ - tm_t0; tm_t0 = t1_; } while (0)
     tm_t0 = __builtin_amdgcn_s_memtime();
 #else
@@ -123,7 +130,8 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
                     s_end = min(s + kp.chunk, kp.spp);
                     part = v3(0, 0, 0);
                     if (unit_pixel(kp, v, px, py)) {
-                        start_path();
+                        new_path();
+                        start_ray();
                     } else {
                         kp.partial[unit] = make_float4(0, 0, 0, 0);
                     }
@@ -137,10 +145,24 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
         for (;;) {
 #ifdef MCPT_PHASE_TIMING
             tm_iters++;
+            {
+                const uint64_t tv = __ballot(mode == kTrav);
+                if (lane == 0) { lu.burst_w += 1; lu.burst_l += (unsigned long long)__popcll(tv); }
+            }
 #endif
             if (mode == kTrav) {
-                if (trav_iter<S>(r, tris, nodes, leafs, st, BLOCK, spill, spill_stride, c))
+                if (trav_iter<S>(r, tris, nodes, leafs, st, BLOCK, spill, spill_stride, c MCPT_LU_ARG)) {
                     mode = kReady;
+#ifndef MCPT_NO_NORMAL_PREFETCH
+                    // start the shading normals' fetch now: it lands while the rest of
+                    // the wave keeps traversing
+                    if (r.htri >= 0) {
+                        nf1 = sc.normals[3 * r.htri];
+                        nf2 = sc.normals[3 * r.htri + 1];
+                        nf3 = sc.normals[3 * r.htri + 2];
+                    }
+#endif
+                }
             }
             const uint64_t trv = __ballot(mode == kTrav);
             const uint64_t rdy = __ballot(mode == kReady);
@@ -150,7 +172,7 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
 
         // ---- shading round for every ready lane (CUTracer.cu:105-175) -------
         if (mode == kReady) {
-            bool done = false;
+            bool done = false, cont = false;
             V3 L = v3(0, 0, 0);
             if constexpr (QE) {
                 // rtx.hlsl:309-370: miss or bounce >= 3*depth ends the path; roulette
@@ -164,10 +186,13 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
                         done = true;
                     } else {
                         c.shades++;
+#ifndef MCPT_NO_NORMAL_PREFETCH
+                        scatter_n(g, nf1, nf2, nf3, r.hbeta, r.hgamma, r.best, 0, sd, color, r.o, r.d);
+#else
                         scatter(g, sc.normals, r.htri, r.hbeta, r.hgamma, r.best, 0, sd, color, r.o, r.d);
+#endif
                         depth++;
-                        c.rays++;
-                        mode = begin_ray(r, sc, kp.best_init) ? kTrav : kReady;
+                        cont = true;
                     }
                 }
             } else if (depth < kp.max_depth) {
@@ -181,10 +206,13 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
                         done = true;
                     } else {
                         c.shades++;
+#ifndef MCPT_NO_NORMAL_PREFETCH
+                        scatter_n(g, nf1, nf2, nf3, r.hbeta, r.hgamma, r.best, kp.fresnel_kd, sd, color, r.o, r.d);
+#else
                         scatter(g, sc.normals, r.htri, r.hbeta, r.hgamma, r.best, kp.fresnel_kd, sd, color, r.o, r.d);
+#endif
                         depth++;
-                        c.rays++;
-                        mode = begin_ray(r, sc, kp.best_init) ? kTrav : kReady;
+                        cont = true;
                     }
                 }
             } else {
@@ -195,6 +223,7 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
                 }
                 done = true;
             }
+            MCPT_STAMP(tm_scatter);
             if (done) {
                 part = vadd(part, L);
                 s++;
@@ -209,9 +238,11 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
                     }
                     mode = kNeed;
                 } else {
-                    start_path();
+                    new_path();
+                    cont = true;
                 }
             }
+            if (cont) start_ray();   // scattered ray or next sample's primary ray
         }
         MCPT_STAMP(tm_shade);
     }
@@ -222,6 +253,16 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
         atomicAdd(kp.stats + 9, tm_trav);
         atomicAdd(kp.stats + 10, tm_shade);
         atomicAdd(kp.stats + 11, tm_iters);
+        atomicAdd(kp.stats + 12, tm_scatter);
+    }
+    {
+        unsigned long long* g = reinterpret_cast<unsigned long long*>(&g_lane_use);
+        const unsigned long long v[6] = {lu.desc_w, lu.desc_l, lu.tri_w, lu.tri_l, lu.burst_w, lu.burst_l};
+        for (int i = 0; i < 6; i++) {
+            unsigned long long x = v[i];
+            for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+            if (lane == 0) atomicAdd(g + i, x);
+        }
     }
 #endif
     flush_counters(c, kp.stats);
@@ -282,6 +323,12 @@ hipError_t launch_render(const KernelParams& kp_in, int cus, hipStream_t st, hip
     if (e != hipSuccess) return e;
     if (ev0) hipEventRecord(ev0, st);
     int variant = 0;
+#ifdef MCPT_EXP_S2   // timing experiment: shallower LDS stack
+    if (true) {
+        variant = 2;
+        e = launch_path<true, 2, kLdsBlock>(kp, cus, lds_bytes_in_lds(img, 2), st);
+    } else
+#endif
     if (lds_bytes_in_lds(img, 8) <= kMaxLds) {
         variant = 1;
         e = launch_path<true, 8, kLdsBlock>(kp, cus, lds_bytes_in_lds(img, 8), st);
@@ -299,6 +346,14 @@ hipError_t launch_render(const KernelParams& kp_in, int cus, hipStream_t st, hip
     if (variant_out) *variant_out = variant;
     return e;
 }
+
+#ifdef MCPT_PHASE_TIMING
+void read_lane_use(unsigned long long out[6]) {   // megakernel lane-use counters, then reset
+    LaneUse z = {0, 0, 0, 0, 0, 0};
+    (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lane_use), sizeof z);
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_lane_use), &z, sizeof z);
+}
+#endif
 
 hipError_t launch_reduce(const KernelParams& kp, float4* fb, hipStream_t st) {
     hipLaunchKernelGGL(reduce_kernel, dim3((kp.npix_local + 255u) / 256u), dim3(256), 0, st, kp, fb);

@@ -102,6 +102,9 @@ int total_lanes_for(uint32_t image_bytes, int cus);
 hipError_t launch_render(const KernelParams& kp, int cus, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1,
                          hipEvent_t ev2, float4* fb, int* variant_out);
 hipError_t launch_reduce(const KernelParams& kp, float4* fb, hipStream_t st);
+#ifdef MCPT_PHASE_TIMING
+void read_lane_use(unsigned long long out[6]);   // diagnostic build only
+#endif
 // wavefront queue segments (= extend workgroups) for a scene image
 int wavefront_segments(uint32_t image_bytes, int cus);
 // wavefront pipeline: generate / extend / shade per bounce / accumulate per

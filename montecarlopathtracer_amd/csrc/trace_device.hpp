@@ -20,6 +20,24 @@ struct Counters {
     uint32_t rays, paths, inner, leaf, refs, tests, shades, spills;
 };
 
+#ifdef MCPT_PHASE_TIMING
+// diagnostic build: executions of a loop body by the wave (w) and by its lanes (l)
+struct LaneUse {
+    unsigned long long desc_w, desc_l, tri_w, tri_l, burst_w, burst_l;
+};
+static __device__ LaneUse g_lane_use;   // summed over waves (diagnostic only)
+__device__ __forceinline__ void lane_use(unsigned long long& w, unsigned long long& l) {
+    const uint64_t ex = __builtin_amdgcn_read_exec();
+    if ((threadIdx.x & 63u) == (uint32_t)(__ffsll((unsigned long long)ex) - 1)) {
+        w += 1;
+        l += (unsigned long long)__popcll(ex);
+    }
+}
+#define MCPT_LANE_USE(wf, lf, acc) lane_use(acc.wf, acc.lf)
+#else
+#define MCPT_LANE_USE(wf, lf, acc) do {} while (0)
+#endif
+
 __device__ __forceinline__ float sel3(int a, float x, float y, float z) {
     return a == 0 ? x : (a == 1 ? y : z);
 }
@@ -39,6 +57,7 @@ struct RayState {
     float tmin, tmax, best;
     uint32_t nw0, nw1, bprio;            // current node record
     int32_t sp, htri;
+    uint32_t lpos, lend;                 // leaf refs still to test (capped leaf loop)
     float hbeta, hgamma;
 };
 
@@ -54,6 +73,7 @@ __device__ __forceinline__ bool begin_ray(RayState& r, const GpuScene& sc, float
     r.nw0 = sc.root_w[0];
     r.nw1 = sc.root_w[1];
     r.sp = 0;
+    r.lpos = r.lend = 0;
     float tmin = 0.0f, tmax = kFltMax;
     const float oo[3] = {r.o.x, r.o.y, r.o.z}, dd[3] = {r.d.x, r.d.y, r.d.z}, inv[3] = {r.ix, r.iy, r.iz};
     bool miss = false;
@@ -117,53 +137,86 @@ __device__ __forceinline__ void test_tri(RayState& r, const float4* __restrict__
 // before the split-plane decision, so the LDS latency overlaps the decision;
 // stack entries carry the far child's record (16 B: w0, w1, lo, hi), so a pop
 // needs no node re-read.
+#ifdef MCPT_PHASE_TIMING
+#define MCPT_LU_PARAM , LaneUse& lu
+#define MCPT_LU_ARG , lu
+#else
+#define MCPT_LU_PARAM
+#define MCPT_LU_ARG
+#endif
+// Descent steps per call are capped at kDescentCap: a lane that has not
+// reached a leaf keeps its node record and interval in RayState and resumes on
+// the next call, so the wave's descent loop is not as long as its deepest
+// lane's (lane use of the uncapped loop: 22%).  Likewise at most kTriCap
+// triangle tests per call, the leaf's remaining refs [lpos, lend) kept in
+// RayState (uncapped leaf loop: 35%).  Same visit order and counts.
+#ifndef MCPT_DESCENT_CAP
+#define MCPT_DESCENT_CAP 5
+#endif
+#ifndef MCPT_TRI_CAP
+#define MCPT_TRI_CAP 2
+#endif
+constexpr int kDescentCap = MCPT_DESCENT_CAP;
+constexpr uint32_t kTriCap = MCPT_TRI_CAP;
 template <int S>
 __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict__ tris,
                                           const uint2* __restrict__ nodes1, const uint32_t* __restrict__ leafs,
                                           uint4* st, int stride, uint4* __restrict__ spill, uint32_t spill_stride,
-                                          Counters& c) {
-    uint32_t w0 = r.nw0, w1 = r.nw1;
-    while ((w0 >> 30) != 3u) {
-        c.inner++;
-        const uint32_t left = w0 & 0x3FFFFFFFu;
-        const uint4 pr = *reinterpret_cast<const uint4*>(nodes1 + left);   // children left, left+1
-        const int a = (int)(w0 >> 30);
-        const float sv = __uint_as_float(w1);
-        const float oa = sel3(a, r.o.x, r.o.y, r.o.z);
-        const float da = sel3(a, r.d.x, r.d.y, r.d.z);
-        const float ia = sel3(a, r.ix, r.iy, r.iz);
-        const float t = (sv - oa) * ia;
-        const bool below = (oa < sv) || (oa == sv && da <= 0.0f);
-        // if/else chain of the oracle, evaluated branch-free
-        const bool pp = (da == 0.0f) & (oa == sv);                  // ray inside the plane: both
-        const bool no = !(t > 0.0f) | (t > r.tmax * kEpsHi);        // near child only
-        const bool fo = t * kEpsHi < r.tmin;                        // far child only
-        const bool go_far = !pp & !no & fo;
-        const bool push_it = pp | (!no & !fo);
-        const uint32_t n0 = below ? pr.x : pr.z, n1 = below ? pr.y : pr.w;     // near child record
-        const uint32_t f0 = below ? pr.z : pr.x, f1 = below ? pr.w : pr.y;     // far child record
-        if (push_it) {
-            const float plo = pp ? r.tmin : (t > r.tmin ? t : r.tmin);
-            uint4* slot = st + (r.sp & (S - 1)) * stride;
-            if (r.sp >= S) {
-                spill[(uint32_t)(r.sp - S) * spill_stride] = *slot;
-                c.spills++;
+                                          Counters& c MCPT_LU_PARAM) {
+    if (r.lpos == r.lend) {                   // between leaves: descend
+        uint32_t w0 = r.nw0, w1 = r.nw1;
+        int steps = 0;
+        while ((w0 >> 30) != 3u) {
+            if (steps == kDescentCap) {       // resume here on the next call
+                r.nw0 = w0;
+                r.nw1 = w1;
+                return false;
             }
-            *slot = make_uint4(f0, f1, __float_as_uint(plo), __float_as_uint(r.tmax));
-            r.sp++;
-            if (!pp) r.tmax = t < r.tmax ? t : r.tmax;
+            steps++;
+            c.inner++;
+            MCPT_LANE_USE(desc_w, desc_l, lu);
+            const uint32_t left = w0 & 0x3FFFFFFFu;
+            const uint4 pr = *reinterpret_cast<const uint4*>(nodes1 + left);   // children left, left+1
+            const int a = (int)(w0 >> 30);
+            const float sv = __uint_as_float(w1);
+            const float oa = sel3(a, r.o.x, r.o.y, r.o.z);
+            const float da = sel3(a, r.d.x, r.d.y, r.d.z);
+            const float ia = sel3(a, r.ix, r.iy, r.iz);
+            const float t = (sv - oa) * ia;
+            const bool below = (oa < sv) | ((oa == sv) & (da <= 0.0f));
+            // if/else chain of the oracle, evaluated branch-free
+            const bool pp = (da == 0.0f) & (oa == sv);                  // ray inside the plane: both
+            const bool no = !(t > 0.0f) | (t > r.tmax * kEpsHi);        // near child only
+            const bool fo = t * kEpsHi < r.tmin;                        // far child only
+            const bool go_far = !pp & !no & fo;
+            const bool push_it = pp | (!no & !fo);
+            const uint32_t n0 = below ? pr.x : pr.z, n1 = below ? pr.y : pr.w;     // near child record
+            const uint32_t f0 = below ? pr.z : pr.x, f1 = below ? pr.w : pr.y;     // far child record
+            if (push_it) {
+                const float plo = pp ? r.tmin : (t > r.tmin ? t : r.tmin);
+                uint4* slot = st + (r.sp & (S - 1)) * stride;
+                if (r.sp >= S) {
+                    spill[(uint32_t)(r.sp - S) * spill_stride] = *slot;
+                    c.spills++;
+                }
+                *slot = make_uint4(f0, f1, __float_as_uint(plo), __float_as_uint(r.tmax));
+                r.sp++;
+                if (!pp) r.tmax = t < r.tmax ? t : r.tmax;
+            }
+            w0 = go_far ? f0 : n0;
+            w1 = go_far ? f1 : n1;
         }
-        w0 = go_far ? f0 : n0;
-        w1 = go_far ? f1 : n1;
+        c.leaf++;
+        r.lpos = w0 & 0x3FFFFFFFu;
+        r.lend = r.lpos + w1;
     }
-    c.leaf++;
-    const uint32_t begin = w0 & 0x3FFFFFFFu;
-    const uint32_t cnt = w1;
-    for (uint32_t i = 0; i < cnt; i++) {
+    for (uint32_t i = 0; i < kTriCap && r.lpos < r.lend; i++, r.lpos++) {
         c.refs++;
+        MCPT_LANE_USE(tri_w, tri_l, lu);
         c.tests++;
-        test_tri(r, tris, leafs[begin + i]);
+        test_tri(r, tris, leafs[r.lpos]);
     }
+    if (r.lpos < r.lend) return false;        // more triangles in this leaf
     if (r.sp == 0) return true;
     r.sp--;
     uint4* slot = st + (r.sp & (S - 1)) * stride;
@@ -217,10 +270,10 @@ __device__ __forceinline__ V3 emitted(V3 color, const GpuGeom& g, float illum) {
 }
 // One scatter event at a non-emitting hit (CUTracer.cu:120-160): interpolated
 // normal, BSDF sample by material, throughput update, next origin/direction.
-__device__ __forceinline__ void scatter(const GpuGeom& g, const float4* __restrict__ normals, int32_t htri,
-                                        float hbeta, float hgamma, float best, int32_t fresnel_kd, uint32_t& sd,
-                                        V3& color, V3& o, V3& d) {
-    const float4 n1 = normals[3 * htri], n2 = normals[3 * htri + 1], n3 = normals[3 * htri + 2];
+// n1..n3 are the hit triangle's vertex normals (fetched by the caller).
+__device__ __forceinline__ void scatter_n(const GpuGeom& g, float4 n1, float4 n2, float4 n3, float hbeta,
+                                          float hgamma, float best, int32_t fresnel_kd, uint32_t& sd, V3& color,
+                                          V3& o, V3& d) {
     V3 nrm = vadd(vadd(vscale(v3(n1.x, n1.y, n1.z), 1.0f - hbeta - hgamma), vscale(v3(n2.x, n2.y, n2.z), hbeta)),
                   vscale(v3(n3.x, n3.y, n3.z), hgamma));
     normalize_cu(nrm);
@@ -233,18 +286,26 @@ __device__ __forceinline__ void scatter(const GpuGeom& g, const float4* __restri
         color = v3(color.x * g.Ks[0], color.y * g.Ks[1], color.z * g.Ks[2]);
     } else {
         color = v3(color.x * g.Kd[0], color.y * g.Kd[1], color.z * g.Kd[2]);
-        if (dot3(dir, nrm) > 0) {
-            const V3 hd = sample_hemi(sd, nrm);
-            dir = v3(-hd.x, -hd.y, -hd.z);
-        } else {
-            dir = sample_hemi(sd, nrm);
-        }
+        // one inlined sampler for both sides (the flip only negates its result)
+        const bool flip = dot3(dir, nrm) > 0;
+        const V3 hd = sample_hemi(sd, nrm);
+        dir = flip ? v3(-hd.x, -hd.y, -hd.z) : hd;
     }
     // hitPoint = pos + t*dir at the accepted t (CUTracer.cu:89-91), then
     // pos = hitPoint + dir*0.01 (:134,143,159)
     const V3 hp = v3(o.x + best * d.x, o.y + best * d.y, o.z + best * d.z);
     o = vadd(hp, vscale(dir, 0.01f));
     d = dir;
+}
+__device__ __forceinline__ void scatter(const GpuGeom& g, const float4* __restrict__ normals, int32_t htri,
+                                        float hbeta, float hgamma, float best, int32_t fresnel_kd, uint32_t& sd,
+                                        V3& color, V3& o, V3& d) {
+#ifdef MCPT_EXP_NONORMAL   // timing experiment only: no global normal fetch (wrong image)
+    const float4 n1 = make_float4(0.0f, 1.0f, 0.0f, 0.0f), n2 = n1, n3 = make_float4(hbeta, 1.0f, hgamma, 0.0f);
+#else
+    const float4 n1 = normals[3 * htri], n2 = normals[3 * htri + 1], n3 = normals[3 * htri + 2];
+#endif
+    scatter_n(g, n1, n2, n3, hbeta, hgamma, best, fresnel_kd, sd, color, o, d);
 }
 // material class of a geometry for the wavefront's per-material queues
 __device__ __forceinline__ uint32_t material_class(const GpuGeom& g) {

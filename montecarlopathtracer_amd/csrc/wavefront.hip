@@ -212,6 +212,9 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
     float4* hit = wf.hit + seg0;
 
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0};
+#ifdef MCPT_PHASE_TIMING
+    LaneUse lu = {0, 0, 0, 0, 0, 0};
+#endif
     SlotCursor cur_chunk = {0, kChunk};
     ClassBuf out[4] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
     RayState r;
@@ -237,7 +240,7 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
         // ---- traversal burst until enough lanes are done ---------------------
         for (;;) {
             if (mode == kTrav) {
-                if (trav_iter<S>(r, tris, nodes, leafs, st, BLOCK, spill, spill_stride, c)) mode = kReady;
+                if (trav_iter<S>(r, tris, nodes, leafs, st, BLOCK, spill, spill_stride, c MCPT_LU_ARG)) mode = kReady;
             }
             const uint64_t trv = __ballot(mode == kTrav);
             const uint64_t rdy = __ballot(mode == kReady);
