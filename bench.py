@@ -37,6 +37,24 @@ def algorithmic_bytes(st: dict, pixels: int) -> dict:
     return {"survey": survey, "own": own}
 
 
+def pmc_traffic(workload: str, pipeline: str):
+    """HBM bytes per path-kernel launch (GB) from the committed rocprofv3 PMC passes
+    (profiles/<round>/pmc_summary.json: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE,
+    scripts/profile_round.sh) when they were taken on this workload; else None."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_summary.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+            bl = d.get("bench_line") or {}
+            if bl.get("config", {}).get("workload") == workload and \
+                    bl.get("config", {}).get("pipeline", "megakernel") == pipeline:
+                g = d["derived"]
+                return round(g["hbm_read_GB_corrected_x2"] + g["hbm_write_GB"], 3), os.path.relpath(f, ROOT)
+        except (OSError, ValueError, KeyError):
+            continue
+    return None, None
+
+
 def cpu_baseline(scene_name: str, width: int, height: int, seconds: float) -> dict:
     """Reference CPU path = the oracle (C restatement of CUTracer.cu + the reference
     KD traversal rtx.hlsl:84-211), single thread, on a bounded centred crop."""
@@ -154,12 +172,15 @@ def main():
         achieved = ab["survey"] / (kern_ms * 1e-3) / 1e9
         achieved_own = ab["own"] / (kern_ms * 1e-3) / 1e9
         mray = rays / elapsed / 1e6
+        workload = f"cornell_{args.width}x{args.height}_{args.spp}spp" + ("" if args.scene == "scene01" else
+                                                                            f"_{args.scene}")
+        traffic, traffic_src = pmc_traffic(workload, args.pipeline)
         line = {
             "metric": METRIC, "value": round(mray, 3), "unit": "Mray/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f32",
             "data": f"bundled reference scene {args.scene}.obj (Cornell Box), synthetic camera/seed",
-            "config": {"workload": f"cornell_{args.width}x{args.height}_{args.spp}spp", "scene": args.scene,
+            "config": {"workload": workload, "scene": args.scene,
                        "width": args.width, "height": args.height, "spp": args.spp, "max_depth": 7,
                        "spp_chunk": args.spp_chunk, "parallelism": f"pixel-tiles x{world}" +
                        (" + rccl gather" if world > 1 else ""), "pipeline": args.pipeline,
@@ -170,7 +191,8 @@ def main():
             "kernel_ms_avg": round(kern_ms, 3),
             "gpu_ms_per_step_event": round(ev0.elapsed_time(ev1) / args.steps, 3),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "traffic_unit": "GB per launch (HBM read+write, rocprofv3 PMC)", "traffic_source": traffic_src,
                          "bytes_model": "SURVEY 8(d): 32*nodes+4*leafrefs+48*tris+96*shades+16*px",
                          "achieved_own_layout": round(achieved_own, 1),
                          "bytes_per_ray": round(ab["survey"] / max(per_launch["rays"], 1), 1),
