@@ -72,6 +72,7 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
     LaneUse lu = {0, 0, 0, 0, 0, 0};
 #endif
     int mode = kNeed;
+    SlotCursor units = {0, kChunk};
     uint32_t s = 0, s_end = 0, unit_id = 0;
     int px = 0, py = 0, depth = 0;
     uint32_t sd = 1;
@@ -111,14 +112,9 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
     for (;;) {
         // ---- work units: one atomic per wave for every lane that needs one ----
         for (;;) {
-            const uint64_t m = __ballot(mode == kNeed);
-            if (!m) break;
-            const int leader = __ffsll((unsigned long long)m) - 1;
-            uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(kp.counter, (uint32_t)__popcll(m));
-            base = __shfl(base, leader);
+            if (!__ballot(mode == kNeed)) break;
+            const uint32_t unit = units.take(mode == kNeed, kp.counter);   // 64 units per atomic
             if (mode == kNeed) {
-                const uint32_t unit = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
                 if (unit >= kp.total_units) {
                     mode = kDead;
                 } else {

@@ -327,6 +327,33 @@ __device__ __forceinline__ uint32_t wave_append(bool want, uint32_t* counter) {
     }
     return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
 }
+constexpr uint32_t kChunk = 64;           // indices a wave reserves at once
+// Wave-level reservation: lanes with `want` get consecutive indices from the
+// wave's current 64-index chunk of a shared counter (LDS or global), one
+// atomic per 64 indices instead of one per refill.
+struct SlotCursor {
+    uint32_t base, used;
+    __device__ __forceinline__ uint32_t take(bool want, uint32_t* counter) {
+        const uint64_t m = __ballot(want);
+        const uint32_t n = (uint32_t)__popcll(m);
+        const int lane = (int)(threadIdx.x & 63u);
+        const uint32_t rank = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        uint32_t res = base + used + rank;
+        if (used + n > kChunk) {                       // wave-uniform
+            const uint32_t first = kChunk - used;
+            uint32_t nb = 0;
+            if (lane == 0) nb = atomicAdd(counter, kChunk);
+            nb = __shfl(nb, 0);
+            if (rank >= first) res = nb + (rank - first);
+            base = nb;
+            used = n - first;
+        } else {
+            used += n;
+        }
+        return res;
+    }
+};
+
 // counters: wave reduction, one atomic per wave per counter
 __device__ __forceinline__ void flush_counters(const Counters& c, unsigned long long* stats) {
     uint32_t vals[8] = {c.rays, c.paths, c.inner, c.leaf, c.refs, c.tests, c.shades, c.spills};

@@ -51,7 +51,6 @@ constexpr int kClassTerminate = 0;
 // queue slot without a ray (pixel outside the image): it ends as a miss with
 // zero radiance and is counted nowhere, like the megakernel's empty units.
 constexpr uint32_t kNoRay = 0xFFFFFFFFu;
-constexpr uint32_t kChunk = 64;           // queue slots a wave reserves at once
 
 __device__ __forceinline__ float4 pack(V3 v, uint32_t w) { return make_float4(v.x, v.y, v.z, __uint_as_float(w)); }
 __device__ __forceinline__ V3 xyz(float4 v) { return v3(v.x, v.y, v.z); }
@@ -98,31 +97,6 @@ __global__ void __launch_bounds__(kGenBlock) wf_generate(const KernelParams kp, 
     }
     flush_counters(c, kp.stats);
 }
-
-// Wave-level slot reservation: lanes with `want` get consecutive queue slots
-// from the wave's current 64-slot chunk, one LDS atomic per 64 slots.
-struct SlotCursor {
-    uint32_t base, used;
-    __device__ __forceinline__ uint32_t take(bool want, uint32_t* counter) {
-        const uint64_t m = __ballot(want);
-        const uint32_t n = (uint32_t)__popcll(m);
-        const int lane = (int)(threadIdx.x & 63u);
-        const uint32_t rank = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-        uint32_t res = base + used + rank;
-        if (used + n > kChunk) {                       // wave-uniform
-            const uint32_t first = kChunk - used;
-            uint32_t nb = 0;
-            if (lane == 0) nb = atomicAdd(counter, kChunk);
-            nb = __shfl(nb, 0);
-            if (rank >= first) res = nb + (rank - first);
-            base = nb;
-            used = n - first;
-        } else {
-            used += n;
-        }
-        return res;
-    }
-};
 
 // Per-class output buffer held in registers: lane j holds entry j of the
 // wave's pending 64-entry block; full blocks go out with one LDS atomic and
