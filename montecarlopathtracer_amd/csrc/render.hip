@@ -33,8 +33,10 @@ using namespace trace;
 
 namespace {
 
+// 4 waves per SIMD (16 per CU) in both layouts: <= 128 VGPRs (the global
+// variant once drifted to 130 and lost a quarter of its occupancy: C4 -20%)
 template <bool IN_LDS, int S, int BLOCK, bool DBG, bool QE>
-__global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
+__global__ void __launch_bounds__(BLOCK, 4) path_kernel(const KernelParams kp) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = (int)threadIdx.x;
     const int lane = tid & 63;
@@ -77,7 +79,6 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
     int px = 0, py = 0, depth = 0;
     uint32_t sd = 1;
     V3 part = v3(0, 0, 0), color = v3(1, 1, 1);
-    float4 nf1 = make_float4(0, 0, 0, 0), nf2 = nf1, nf3 = nf1;   // prefetched shading normals
     RayState r;
     r.o = eye;
     r.d = v3(0, 0, -1);
@@ -112,8 +113,19 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
     for (;;) {
         // ---- work units: one atomic per wave for every lane that needs one ----
         for (;;) {
-            if (!__ballot(mode == kNeed)) break;
-            const uint32_t unit = units.take(mode == kNeed, kp.counter);   // 64 units per atomic
+            const uint64_t m = __ballot(mode == kNeed);
+            if (!m) break;
+            uint32_t unit;
+            if constexpr (IN_LDS) {
+                unit = units.take(mode == kNeed, kp.counter);   // 64 units per atomic
+            } else {
+                // scenes in global memory: units strictly in global order, one atomic
+                // per refill (C4 1.94 vs 1.69 G rays/s with 64-unit wave chunks)
+                const int leader = __ffsll((unsigned long long)m) - 1;
+                uint32_t base = 0;
+                if (lane == leader) base = atomicAdd(kp.counter, (uint32_t)__popcll(m));
+                unit = __shfl(base, leader) + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+            }
             if (mode == kNeed) {
                 if (unit >= kp.total_units) {
                     mode = kDead;
@@ -147,18 +159,8 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
             }
 #endif
             if (mode == kTrav) {
-                if (trav_iter<S>(r, tris, nodes, leafs, st, BLOCK, spill, spill_stride, c MCPT_LU_ARG)) {
+                if (trav_iter<S>(r, tris, nodes, leafs, st, BLOCK, spill, spill_stride, c MCPT_LU_ARG))
                     mode = kReady;
-#ifndef MCPT_NO_NORMAL_PREFETCH
-                    // start the shading normals' fetch now: it lands while the rest of
-                    // the wave keeps traversing
-                    if (r.htri >= 0) {
-                        nf1 = sc.normals[3 * r.htri];
-                        nf2 = sc.normals[3 * r.htri + 1];
-                        nf3 = sc.normals[3 * r.htri + 2];
-                    }
-#endif
-                }
             }
             const uint64_t trv = __ballot(mode == kTrav);
             const uint64_t rdy = __ballot(mode == kReady);
@@ -182,11 +184,7 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
                         done = true;
                     } else {
                         c.shades++;
-#ifndef MCPT_NO_NORMAL_PREFETCH
-                        scatter_n(g, nf1, nf2, nf3, r.hbeta, r.hgamma, r.best, 0, sd, color, r.o, r.d);
-#else
                         scatter(g, sc.normals, r.htri, r.hbeta, r.hgamma, r.best, 0, sd, color, r.o, r.d);
-#endif
                         depth++;
                         cont = true;
                     }
@@ -202,11 +200,7 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
                         done = true;
                     } else {
                         c.shades++;
-#ifndef MCPT_NO_NORMAL_PREFETCH
-                        scatter_n(g, nf1, nf2, nf3, r.hbeta, r.hgamma, r.best, kp.fresnel_kd, sd, color, r.o, r.d);
-#else
                         scatter(g, sc.normals, r.htri, r.hbeta, r.hgamma, r.best, kp.fresnel_kd, sd, color, r.o, r.d);
-#endif
                         depth++;
                         cont = true;
                     }

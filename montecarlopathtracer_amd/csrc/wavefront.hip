@@ -52,6 +52,11 @@ constexpr int kClassTerminate = 0;
 // zero radiance and is counted nowhere, like the megakernel's empty units.
 constexpr uint32_t kNoRay = 0xFFFFFFFFu;
 
+__device__ __forceinline__ float opaque(float x) {
+    float y;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(y) : "v"(x));
+    return y;
+}
 __device__ __forceinline__ float4 pack(V3 v, uint32_t w) { return make_float4(v.x, v.y, v.z, __uint_as_float(w)); }
 __device__ __forceinline__ V3 xyz(float4 v) { return v3(v.x, v.y, v.z); }
 
@@ -198,8 +203,11 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
     uint32_t nslot = cur_chunk.take(true, lcnt + 4);
     float4 no4 = make_float4(0, 0, 0, 0), nd4 = make_float4(0, 0, 0, 0);
     auto start = [&](float4 o4, float4 d4) {
-        r.o = xyz(o4);
-        r.d = xyz(d4);
+        // opaque copies: the loop below must not see its ray registers as
+        // memory-loaded, or LLVM flushes vmcnt in the descent loop's preheader
+        // (the loop holds the spill store) and waits for the next-ray prefetch
+        r.o = v3(opaque(o4.x), opaque(o4.y), opaque(o4.z));
+        r.d = v3(opaque(d4.x), opaque(d4.y), opaque(d4.z));
         depth = __float_as_uint(d4.w);
         if (depth == kNoRay) {
             r.htri = -1;
