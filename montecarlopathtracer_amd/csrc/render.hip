@@ -33,10 +33,12 @@ using namespace trace;
 
 namespace {
 
-// 4 waves per SIMD (16 per CU) in both layouts: <= 128 VGPRs (the global
-// variant once drifted to 130 and lost a quarter of its occupancy: C4 -20%)
+// Both layouts run 16 waves per CU and need <= 128 VGPRs; keep an eye on the
+// global variant (at 130 it lost a quarter of its occupancy: C4 -20%).  An
+// explicit min-waves bound (__launch_bounds__(BLOCK, 4)) made it slower (C4
+// 1.81 vs 1.97 G rays/s), so the budget is kept by the code instead.
 template <bool IN_LDS, int S, int BLOCK, bool DBG, bool QE>
-__global__ void __launch_bounds__(BLOCK, 4) path_kernel(const KernelParams kp) {
+__global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = (int)threadIdx.x;
     const int lane = tid & 63;
