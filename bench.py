@@ -55,15 +55,16 @@ def pmc_traffic(workload: str, pipeline: str):
     return None, None
 
 
-def cpu_baseline(scene_name: str, width: int, height: int, seconds: float) -> dict:
+def cpu_baseline(scene_name: str, width: int, height: int, seconds: float, threads: int) -> dict:
     """Reference CPU path = the oracle (C restatement of CUTracer.cu + the reference
-    KD traversal rtx.hlsl:84-211), single thread, on a bounded centred crop."""
+    KD traversal rtx.hlsl:84-211, pthreads over rows) on `threads` host cores, on a
+    bounded sample of the workload: centred crops rendered until `seconds` pass."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # test/bench infrastructure only
     from montecarlopathtracer_amd.scenes import scene_path
     oracle.build()
     s = oracle.Scene(scene_path(scene_name))
-    crop = 64
+    crop = 64 if threads == 1 else 256
     spp = 8
     total_rays, total_t = 0, 0.0
     runs = 0
@@ -71,15 +72,25 @@ def cpu_baseline(scene_name: str, width: int, height: int, seconds: float) -> di
         x0 = (width - crop) // 2 + (runs % 4) * 8
         y0 = (height - crop) // 2 + (runs // 4 % 4) * 8
         p = oracle.RenderParams(width=width, height=height, spp=spp, spp_chunk=32, spp_offset=runs * spp,
-                                traversal=oracle.KD_REF, threads=1, region=(x0, y0, x0 + crop, y0 + crop))
+                                traversal=oracle.KD_REF, threads=threads, region=(x0, y0, x0 + crop, y0 + crop))
         t0 = time.perf_counter()
         _, c = s.render(p)
         total_t += time.perf_counter() - t0
         total_rays += c["rays"]
         runs += 1
-    return {"value": round(total_rays / total_t / 1e6, 4), "unit": "Mray/s", "cores": 1, "kind": "port",
+    return {"value": round(total_rays / total_t / 1e6, 4), "unit": "Mray/s", "cores": threads, "kind": "port",
             "sample": f"{runs} x ({crop}x{crop} centred crop, {spp} spp) of {scene_name} {width}x{height}, "
-                      f"{total_rays} rays in {total_t:.1f}s, oracle traversal=KD_REF (rtx.hlsl order), 1 thread"}
+                      f"{total_rays} rays in {total_t:.1f}s, oracle traversal=KD_REF (rtx.hlsl order), "
+                      f"{threads} thread(s)"}
+
+
+def host_cores() -> int:
+    """CPU share of this process (the GPU box gives 16 per GPU; os.cpu_count() shows the host)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(n, int(os.environ.get("OMP_NUM_THREADS", "16"))))
 
 
 def main():
@@ -95,6 +106,7 @@ def main():
     ap.add_argument("--pipeline", choices=["megakernel", "wavefront"], default="megakernel")
     ap.add_argument("--wf-batch", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = this process's CPU share (<= 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -201,7 +213,8 @@ def main():
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(args.scene, args.width, args.height, args.cpu_seconds)
+            line["cpu_baseline"] = cpu_baseline(args.scene, args.width, args.height, args.cpu_seconds,
+                                                args.cpu_threads or host_cores())
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
