@@ -17,7 +17,7 @@ CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIBDIR, os.environ.get("MCPT_LIB_NAME", "libmcpt.so"))
 SOURCES = ["host_model.cpp", "capi.cpp", "render.hip", "wavefront.hip"]
-HEADERS = ["host_model.hpp", "mcpt_device.hpp", "render_launch.hpp", "trace_device.hpp"]
+HEADERS = ["host_model.hpp", "mcpt_device.hpp", "render_launch.hpp", "trace_device.hpp", "half_box.hpp"]
 ARCH = os.environ.get("MCPT_OFFLOAD_ARCH", "gfx950")
 
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-fno-slp-vectorize", "-Wall",

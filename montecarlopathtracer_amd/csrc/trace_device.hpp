@@ -158,11 +158,39 @@ __device__ __forceinline__ void test_tri(RayState& r, const float4* __restrict__
 #endif
 constexpr int kDescentCap = MCPT_DESCENT_CAP;
 constexpr uint32_t kTriCap = MCPT_TRI_CAP;
-template <int S>
+// Leaf box cull (scenes in global memory): the leaf's KD box, stored as fp16
+// rounded outward (half_box.hpp), against the ray segment (0, best].  A hit
+// at t in (0, best] lies inside the exact box, hence inside the stored one,
+// and its slabs contain t up to rounding, which the 2^-12 margins cover: the
+// cull never drops a hit that could improve `best`.
+__device__ __forceinline__ float h2f(uint32_t bits16) {
+    return (float)__builtin_bit_cast(_Float16, (unsigned short)bits16);
+}
+__device__ __forceinline__ void box_slab(float o, float d, float inv, float blo, float bhi, float& lo, float& hi,
+                                         bool& out) {
+    if (d == 0.0f) {
+        out = out | (o < blo) | (o > bhi);
+    } else {
+        const float t0 = (blo - o) * inv, t1 = (bhi - o) * inv;
+        const float a0 = t0 < t1 ? t0 : t1, a1 = t0 < t1 ? t1 : t0;
+        lo = a0 > lo ? a0 : lo;
+        hi = a1 < hi ? a1 : hi;
+    }
+}
+__device__ __forceinline__ bool leaf_box_hit(const RayState& r, uint4 rb) {
+    float lo = 0.0f, hi = r.best;
+    bool out = false;
+    box_slab(r.o.x, r.d.x, r.ix, h2f(rb.x & 0xFFFFu), h2f(rb.y >> 16), lo, hi, out);
+    box_slab(r.o.y, r.d.y, r.iy, h2f(rb.x >> 16), h2f(rb.z & 0xFFFFu), lo, hi, out);
+    box_slab(r.o.z, r.d.z, r.iz, h2f(rb.y & 0xFFFFu), h2f(rb.z >> 16), lo, hi, out);
+    return !out && !(lo * kEpsLo > hi * kEpsHi);
+}
+
+template <int S, bool BOXES = false>
 __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict__ tris,
                                           const uint2* __restrict__ nodes1, const uint32_t* __restrict__ leafs,
                                           uint4* st, int stride, uint4* __restrict__ spill, uint32_t spill_stride,
-                                          Counters& c MCPT_LU_PARAM) {
+                                          Counters& c MCPT_LU_PARAM, const uint4* __restrict__ lboxes = nullptr) {
     if (r.lpos == r.lend) {                   // between leaves: descend
         uint32_t w0 = r.nw0, w1 = r.nw1;
         int steps = 0;
@@ -208,7 +236,12 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
         }
         c.leaf++;
         r.lpos = w0 & 0x3FFFFFFFu;
-        r.lend = r.lpos + w1;
+        uint32_t cnt = w1;
+        if constexpr (BOXES) {                // y word = leaf ordinal; count in the box record
+            const uint4 rb = lboxes[w1];
+            cnt = leaf_box_hit(r, rb) ? rb.w : 0u;
+        }
+        r.lend = r.lpos + cnt;
     }
     for (uint32_t i = 0; i < kTriCap && r.lpos < r.lend; i++, r.lpos++) {
         c.refs++;

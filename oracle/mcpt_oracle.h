@@ -68,6 +68,8 @@ typedef struct {
                                        0: no tint (rtx.hlsl:345, the published renders) */
     int32_t mode;                   /* 0: CVMCTracer semantics; 1: QuinEngine (rtx.hlsl:304-405) */
     float proj11, proj22;           /* QE: PerspectiveFovRH scales (orc_qe_proj)  */
+    int32_t leaf_boxes;             /* ordered KD: cull leaves by their fp16 KD box (the
+                                       kernel does for scenes served from global memory) */
 } orc_params;
 
 typedef struct {
@@ -115,6 +117,9 @@ void orc_sample_hemi(const float* n, const float* u, float* out);
 void orc_sample_phong(const float* n, const float* in, uint32_t Ns, const float* u, float* out);
 void orc_sample_fresnel(const float* n, const float* in, float Tr, float Ni, const float* u, float* out);
 float orc_tan_half_fov(float fov_deg);
+/* binary16 of x rounded toward -inf (dir < 0) / +inf (dir > 0), and back */
+uint16_t orc_f16_dir(float x, int dir);
+float orc_f16_to_f32(uint16_t h);
 /* QE camera (GraphicsRTX.cpp:181-182): D3DXMatrixPerspectiveFovRH(fovY, W/H) diagonal */
 void orc_qe_proj(float fovy_deg, int32_t width, int32_t height, float* p11, float* p22);
 void orc_camera_basis(const float* eye, const float* dir, const float* up,

@@ -294,6 +294,7 @@ typedef struct {
     const orc_scene* s;
     const orc_v3 (*kv)[3];   /* vertices by kd id */
     int traversal;
+    int leaf_boxes;          /* ordered walk: fp16 leaf-box cull */
     float best_init;         /* FLT_MAX (CUTracer.cu:46); 10000 in QE mode (rtx.hlsl:88) */
     orc_counters c;
 } qctx;
@@ -402,6 +403,59 @@ static hit_t isect_kd_ref(qctx* q, orc_v3 o, orc_v3 d) {
 
 /* Ordered front-to-back traversal used by the HIP kernel:
  * split-plane intervals, conservative 2^-12 margins, full stack (<= depth). */
+
+/* ====================== fp16 leaf boxes (kernel mirror) =================== */
+float orc_f16_to_f32(uint16_t h) {
+    uint32_t sg = (h >> 15) & 1u, e = (h >> 10) & 0x1Fu, m = h & 0x3FFu;
+    if (e == 0) {
+        float v = (float)m * 5.9604644775390625e-8f;
+        return sg ? -v : v;
+    }
+    uint32_t bits = e == 31 ? ((sg << 31) | 0x7F800000u | (m << 13)) : ((sg << 31) | ((e - 15u + 127u) << 23) | (m << 13));
+    float f;
+    memcpy(&f, &bits, 4);
+    return f;
+}
+uint16_t orc_f16_dir(float x, int dir) {
+    uint32_t u;
+    memcpy(&u, &x, 4);
+    uint32_t sg = u >> 31, mag;
+    float a = x < 0 ? -x : x;
+    if (!(a < 65520.0f)) {
+        mag = 0x7C00u;
+    } else if (a < 6.103515625e-05f) {
+        mag = (uint32_t)(a * 16777216.0f);
+    } else {
+        uint32_t ua;
+        memcpy(&ua, &a, 4);
+        mag = (((ua >> 23) - 127u + 15u) << 10) | ((ua >> 13) & 0x3FFu);
+        if (mag > 0x7BFFu) mag = 0x7BFFu;
+    }
+    int up = sg ? dir < 0 : dir > 0;
+    if (mag < 0x7C00u && orc_f16_to_f32((uint16_t)mag) != a && up) mag += 1u;
+    if (mag >= 0x7C00u && !up) mag = 0x7BFFu;
+    if (mag == 0 && sg) return (uint16_t)0x8000u;
+    return (uint16_t)((sg << 15) | mag);
+}
+/* does the ray segment (0, best] meet the leaf's fp16 box?  (trace_device.hpp leaf_box_hit) */
+static int leaf_box_hit(const orc_node* nd, const float* oo, const float* dd, const float* inv, float best) {
+    float lo = 0.0f, hi = best;
+    int out = 0;
+    for (int a = 0; a < 3; a++) {
+        float blo = orc_f16_to_f32(orc_f16_dir(nd->bmin[a], -1));
+        float bhi = orc_f16_to_f32(orc_f16_dir(nd->bmax[a], +1));
+        if (dd[a] == 0.0f) {
+            out |= (oo[a] < blo) | (oo[a] > bhi);
+        } else {
+            float t0 = (blo - oo[a]) * inv[a], t1 = (bhi - oo[a]) * inv[a];
+            float a0 = t0 < t1 ? t0 : t1, a1 = t0 < t1 ? t1 : t0;
+            lo = a0 > lo ? a0 : lo;
+            hi = a1 < hi ? a1 : hi;
+        }
+    }
+    return !out && !(lo * KD_EPS_LO > hi * KD_EPS_HI);
+}
+
 static hit_t isect_kd_ordered(qctx* q, orc_v3 o, orc_v3 d) {
     const orc_scene* s = q->s;
     hit_t h;
@@ -456,7 +510,9 @@ static hit_t isect_kd_ordered(qctx* q, orc_v3 o, orc_v3 d) {
             nd = &s->nodes[node];
         }
         q->c.leaf_visits++;
-        for (uint32_t i = 0; i < nd->tri_count; i++) {
+        uint32_t cnt = nd->tri_count;
+        if (q->leaf_boxes && !leaf_box_hit(nd, oo, dd, inv, best)) cnt = 0;
+        for (uint32_t i = 0; i < cnt; i++) {
             uint32_t k = s->leaf_ids[nd->tri_begin + i];
             q->c.leaf_refs++;
             q->c.tri_tests++;
@@ -720,6 +776,7 @@ static void* render_worker(void* arg) {
     q.s = j->s;
     q.kv = j->kv;
     q.traversal = p->traversal;
+    q.leaf_boxes = p->leaf_boxes;
     q.best_init = p->mode == 1 ? QE_T_BEST : FLT_MAX;
     uint32_t key = orc_seed_key(p->seed);
     for (;;) {

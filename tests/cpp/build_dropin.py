@@ -3,13 +3,14 @@
 pw_tracer_dropin  include/mcpt_pw_tracer.hpp: the CVMCTracer main.cpp call sequence
 qe_viewer         include/mcpt_qe_viewer.hpp: the QuinEngine OnUpdate frame loop
 image_io          include/mcpt_image_io.hpp: the main.cpp:19-29 encode, PNG and PFM
+half_box_probe    csrc/half_box.hpp: the outward-rounded fp16 leaf boxes (vs the oracle's)
 """
 import os
 import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
-LINKS_MCPT = {"pw_tracer_dropin": True, "qe_viewer": True, "image_io": False}
+LINKS_MCPT = {"pw_tracer_dropin": True, "qe_viewer": True, "image_io": False, "half_box_probe": False}
 
 
 def build(name: str = "pw_tracer_dropin") -> str:

@@ -196,3 +196,46 @@ def test_quinengine_mode_brute_equals_kd_and_is_gamma_encoded(oracle_mod, mcpt):
     # depth 0: roulette from the first hit; with max_depth 1 paths are capped at 3 bounces
     c, cc = s.render(oracle_mod.RenderParams(traversal=oracle_mod.KD_ORDERED, **dict(kw, max_depth=1)))
     assert cc["rays"] <= 4 * cc["paths"]
+
+
+def test_leaf_box_cull_is_exact_and_prunes(oracle_mod, mcpt):
+    """The fp16 leaf-box cull the kernel applies to scenes in global memory:
+    identical images with it on and off; most triangle tests disappear."""
+    for name, sid in (("scene01", 1), ("scene02", 2), ("scene03", 2)):
+        s = oracle_mod.Scene(mcpt.scene_path(name))
+        kw = dict(width=40, height=30, spp=3, threads=8, scene_id=sid, traversal=oracle_mod.KD_ORDERED)
+        a, ca = s.render(oracle_mod.RenderParams(leaf_boxes=0, **kw))
+        b, cb = s.render(oracle_mod.RenderParams(leaf_boxes=1, **kw))
+        assert np.array_equal(a, b), name
+        assert ca["rays"] == cb["rays"] and ca["inner_visits"] == cb["inner_visits"]
+        assert cb["tri_tests"] <= ca["tri_tests"]
+        if name != "scene03":   # scene03 from camera 2: few leaves, all of them hit
+            assert cb["tri_tests"] < 0.5 * ca["tri_tests"], (name, ca["tri_tests"], cb["tri_tests"])
+
+
+def test_fp16_box_rounding_contains_and_matches_product(oracle_mod, tmp_path):
+    """orc_f16_dir (oracle) == mcpt::f32_to_f16_dir (csrc/half_box.hpp) bit for bit,
+    and the rounded values bracket the input."""
+    import ctypes as C
+    import subprocess
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "cpp"))
+    import build_dropin
+    r = np.random.default_rng(7)
+    x = np.concatenate([r.uniform(-20, 20, 20000), r.standard_normal(5000) * 1e-5,
+                        np.ldexp(r.uniform(-1, 1, 5000), r.integers(-30, 20, 5000)),
+                        [0.0, -0.0, 65504, 65519, 65520, -65520, 1e9, -1e9, 6.1035e-5, 5.9604645e-8]]).astype(np.float32)
+    src, dst = tmp_path / "x.f32", tmp_path / "h.u16"
+    x.tofile(src)
+    exe = build_dropin.build("half_box_probe")
+    out = subprocess.run([exe, str(src), str(x.size), str(dst)], capture_output=True, text=True)
+    assert out.returncode == 0, out.stderr
+    prod = np.fromfile(dst, np.uint16).reshape(-1, 2)
+    L = oracle_mod.lib()
+    L.orc_f16_dir.restype = C.c_uint16
+    L.orc_f16_dir.argtypes = [C.c_float, C.c_int]
+    ref = np.array([[L.orc_f16_dir(float(v), -1), L.orc_f16_dir(float(v), 1)] for v in x], np.uint16)
+    assert np.array_equal(prod, ref)
+    lo = ref[:, 0].view(np.float16).astype(np.float32)
+    hi = ref[:, 1].view(np.float16).astype(np.float32)
+    assert np.all(lo <= x) and np.all(hi >= x)
