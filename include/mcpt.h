@@ -65,7 +65,7 @@ typedef struct {
     int64_t kd_depth;      /* deepest node depth (<= 32) */
     int64_t lds_bytes;     /* LDS image size; 0 if the scene is served from global memory */
     int64_t device;        /* HIP device ordinal holding the scene */
-    int64_t leaf_boxes;    /* 1: served from global memory, leaves culled by their KD boxes */
+    int64_t node_boxes;    /* 1: served from global memory, children culled by their KD boxes */
 } mcpt_scene_info;
 
 typedef struct {

@@ -43,7 +43,7 @@ class ModelInfo(C.Structure):
 class SceneInfo(C.Structure):
     _fields_ = [(n, C.c_int64) for n in
                 ("n_geometries", "n_triangles", "n_nodes", "n_leaf_refs", "kd_depth", "lds_bytes", "device",
-                 "leaf_boxes")]
+                 "node_boxes")]
 
 
 class RenderParamsC(C.Structure):

@@ -208,25 +208,25 @@ void build_image(mcpt_scene& s) {
             throw mcpt::Error{MCPT_E_INVALID, "KD sibling pair not at an odd index"};
     auto al16 = [](size_t x) { return (x + 15u) & ~size_t(15); };
     auto al128 = [](size_t x) { return (x + 127u) & ~size_t(127); };
-    // scenes that fit in LDS keep the packed order (no cache lines there, every
-    // byte counts); larger ones get line-aligned clusters
+    // Scenes that fit in LDS: 8-B node records in packed cluster order (every
+    // LDS byte counts).  Larger scenes: 48-B sibling-pair records -- the two
+    // node words plus both children's KD boxes as fp16 rounded outward, so the
+    // traversal skips children the ray misses (child-box cull).
     DeviceOrder ord = device_order(hs, false);
-    // leaf box records (global-memory scenes only): 6 x fp16 box + u32 count
     bool boxes = false;
-    auto image_size = [&](const DeviceOrder& o, size_t& on, size_t& ol, size_t& ob, size_t& og) {
+    auto image_size = [&](const DeviceOrder& o, size_t& on, size_t& ol, size_t& og) {
         on = al128(size_t(nt) * 48);
-        // node slot j = device node j-1 (slot 0 = padding): pairs are aligned 16-B records
-        ol = al16(on + size_t(o.n_slots + 1) * 8);
-        ob = al16(ol + size_t(nl) * 4);
-        og = al16(ob + (boxes ? o.leaf_order.size() * 16 : 0));
+        if (boxes) ol = al16(on + size_t((o.n_slots - 1) / 2) * 48);   // pair m: device nodes 2m+1, 2m+2
+        else ol = al16(on + size_t(o.n_slots + 1) * 8);                 // node slot j = device node j-1
+        og = al16(ol + size_t(nl) * 4);
         return al16(og + size_t(ng) * 64);
     };
-    size_t off_nodes, off_leafs, off_lboxes, off_geoms;
-    size_t total = image_size(ord, off_nodes, off_leafs, off_lboxes, off_geoms);
-    if (mcpt::lds_bytes_in_lds(static_cast<uint32_t>(std::min<size_t>(total, 0xFFFFFFF0u)), 4) + 32 > mcpt::kMaxLds) {
-        ord = device_order(hs, true);
+    size_t off_nodes, off_leafs, off_geoms;
+    size_t total = image_size(ord, off_nodes, off_leafs, off_geoms);
+    if (mcpt::lds_bytes_in_lds(static_cast<uint32_t>(std::min<size_t>(total, 0xFFFFFFF0u)), 4) + 32 > mcpt::kMaxLds ||
+        std::getenv("MCPT_EXP_GLOBAL")) {
         boxes = true;
-        total = image_size(ord, off_nodes, off_leafs, off_lboxes, off_geoms);
+        total = image_size(ord, off_nodes, off_leafs, off_geoms);
     }
     const size_t off_tris = 0;
     if (total > 0xFFFFFFF0u) throw mcpt::Error{MCPT_E_UNSUPPORTED, "scene image exceeds 4 GiB"};
@@ -245,24 +245,11 @@ void build_image(mcpt_scene& s) {
         std::memcpy(img + off_tris + size_t(slot) * 48, rec, 48);
     }
     // leaf references, leaves in device order
-    std::vector<uint32_t> leaf_begin_new(nn, 0), leaf_ordinal(nn, 0);
+    std::vector<uint32_t> leaf_begin_new(nn, 0);
     {
         uint32_t* refs = reinterpret_cast<uint32_t*>(img + off_leafs);
         uint32_t at = 0;
-        uint32_t ordinal = 0;
         for (uint32_t i : ord.leaf_order) {
-            if (boxes) {   // rounded outward: the fp16 box contains the build's box
-                const mcpt::KdNode& n = hs.nodes[i];
-                uint16_t hb[8];
-                for (int a = 0; a < 3; ++a) {
-                    hb[a] = mcpt::f32_to_f16_dir(n.bmin[a], -1);
-                    hb[3 + a] = mcpt::f32_to_f16_dir(n.bmax[a], +1);
-                }
-                const uint32_t cnt = n.leaf_count;
-                std::memcpy(&hb[6], &cnt, 4);
-                std::memcpy(img + off_lboxes + size_t(ordinal) * 16, hb, 16);
-                leaf_ordinal[i] = ordinal++;
-            }
             leaf_begin_new[i] = at;
             for (uint32_t r = 0; r < hs.nodes[i].leaf_count; ++r)
                 refs[at++] = ord.tri_new[hs.leaf_ids[hs.nodes[i].leaf_begin + r]];
@@ -276,10 +263,28 @@ void build_image(mcpt_scene& s) {
             std::memcpy(&w[1], &n.split, 4);
         } else {
             w[0] = (3u << 30) | leaf_begin_new[i];
-            w[1] = boxes ? leaf_ordinal[i] : n.leaf_count;   // with boxes the count is in the box record
+            w[1] = n.leaf_count;
         }
-        std::memcpy(img + off_nodes + size_t(ord.node_new[i] + 1) * 8, w, 8);
-        if (i == 0) { s.gpu.root_w[0] = w[0]; s.gpu.root_w[1] = w[1]; }
+        const uint32_t dv = ord.node_new[i];
+        if (i == 0) {
+            s.gpu.root_w[0] = w[0];
+            s.gpu.root_w[1] = w[1];
+            if (boxes) continue;              // the root has no pair record
+        }
+        if (!boxes) {
+            std::memcpy(img + off_nodes + size_t(dv + 1) * 8, w, 8);
+            continue;
+        }
+        // pair record: [w(left) w(right)] [box(left) box(right)] [pad]; boxes rounded outward
+        const size_t m = (dv - 1) / 2, side = (dv - 1) % 2;
+        unsigned char* rec = img + off_nodes + m * 48;
+        std::memcpy(rec + side * 8, w, 8);
+        uint16_t hb[6];
+        for (int a = 0; a < 3; ++a) {
+            hb[a] = mcpt::f32_to_f16_dir(n.bmin[a], -1);
+            hb[3 + a] = mcpt::f32_to_f16_dir(n.bmax[a], +1);
+        }
+        std::memcpy(rec + 16 + side * 12, hb, 12);
     }
     for (uint32_t g = 0; g < ng; ++g) {
         const mcpt::Geometry& ge = hs.geoms[g];
@@ -297,8 +302,7 @@ void build_image(mcpt_scene& s) {
     gs.off_nodes = static_cast<uint32_t>(off_nodes);
     gs.off_leafs = static_cast<uint32_t>(off_leafs);
     gs.off_geoms = static_cast<uint32_t>(off_geoms);
-    gs.off_lboxes = static_cast<uint32_t>(off_lboxes);
-    gs.leaf_boxes = boxes ? 1u : 0u;
+    gs.node_boxes = boxes ? 1u : 0u;
     gs.n_tris = nt; gs.n_nodes = nn; gs.n_leafs = nl; gs.n_geoms = ng;
     if (nn) {
         for (int a = 0; a < 3; ++a) { gs.root_min[a] = hs.nodes[0].bmin[a]; gs.root_max[a] = hs.nodes[0].bmax[a]; }
@@ -743,8 +747,8 @@ int mcpt_scene_get_info(const mcpt_scene* s, mcpt_scene_info* out) {
     out->n_nodes = static_cast<int64_t>(s->hs.nodes.size());
     out->n_leaf_refs = static_cast<int64_t>(s->hs.leaf_ids.size());
     out->kd_depth = s->hs.kd_depth;
-    out->lds_bytes = s->gpu.leaf_boxes ? 0 : s->gpu.image_bytes;
-    out->leaf_boxes = s->gpu.leaf_boxes;
+    out->lds_bytes = s->gpu.node_boxes ? 0 : s->gpu.image_bytes;
+    out->node_boxes = s->gpu.node_boxes;
     out->device = s->device;
     return MCPT_OK;
 }

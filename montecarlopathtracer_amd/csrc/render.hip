@@ -64,7 +64,7 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
         leafs = reinterpret_cast<const uint32_t*>(sc.image + sc.off_leafs);
         geoms = reinterpret_cast<const GpuGeom*>(sc.image + sc.off_geoms);
     }
-    const uint4* lboxes = reinterpret_cast<const uint4*>(sc.image + sc.off_lboxes);   // global variant only
+    const uint4* pairs = reinterpret_cast<const uint4*>(sc.image + sc.off_nodes);   // 48-B pair records (global variant)
     uint4* st = reinterpret_cast<uint4*>(smem + kp.lds_stack_off) + tid;   // [S][BLOCK] x 16 B
     const uint32_t gl = blockIdx.x * BLOCK + (uint32_t)tid;
     uint4* spill = kp.spill + gl;
@@ -162,7 +162,7 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
             }
 #endif
             if (mode == kTrav) {
-                if (trav_iter<S, !IN_LDS>(r, tris, nodes, leafs, st, BLOCK, spill, spill_stride, c MCPT_LU_ARG, lboxes))
+                if (trav_iter<S, !IN_LDS>(r, tris, nodes, leafs, st, BLOCK, spill, spill_stride, c MCPT_LU_ARG, pairs))
                     mode = kReady;
             }
             const uint64_t trv = __ballot(mode == kTrav);
@@ -310,7 +310,7 @@ hipError_t launch_render(const KernelParams& kp_in, int cus, hipStream_t st, hip
                          hipEvent_t ev2, float4* fb, int* variant_out) {
     KernelParams kp = kp_in;
     const uint32_t img = kp.scene.image_bytes;
-    kp.lds_stack_off = (!kp.scene.leaf_boxes && lds_bytes_in_lds(img, 4) <= kMaxLds) ? img : 0u;
+    kp.lds_stack_off = (!kp.scene.node_boxes && lds_bytes_in_lds(img, 4) <= kMaxLds) ? img : 0u;
     kp.total_lanes = (uint32_t)total_lanes_for(img, cus);
     hipError_t e = hipMemsetAsync(kp.counter, 0, sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
@@ -322,7 +322,7 @@ hipError_t launch_render(const KernelParams& kp_in, int cus, hipStream_t st, hip
         e = launch_path<true, 2, kLdsBlock>(kp, cus, lds_bytes_in_lds(img, 2), st);
     } else
 #endif
-    if (kp.scene.leaf_boxes) {                     // image built for global memory
+    if (kp.scene.node_boxes) {                     // image built for global memory
         variant = 3;
         e = launch_path<false, 8, kGlobalBlock>(kp, cus * kGlobalBlocksPerCu, (size_t)8 * kGlobalBlock * 16, st);
     } else if (lds_bytes_in_lds(img, 8) <= kMaxLds) {

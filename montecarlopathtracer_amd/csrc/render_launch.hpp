@@ -9,9 +9,9 @@
 //          16-B record: inner x = axis<<30 | left child, y = split value bits;
 //          leaf x = 3<<30 | first leaf ref, y = count                       8 B
 //   leafs  uint32 KD triangle id per leaf reference                    4 B
-//   lboxes (scenes too large for LDS) per leaf: its KD box as 6 x fp16
-//          rounded outward + u32 triangle count; the leaf node's y word
-//          then holds the leaf's ordinal instead of the count              16 B
+//   (scenes too large for LDS: nodes are 48-B sibling-pair records instead,
+//          the two node words + both children's KD boxes as 6 x fp16
+//          rounded outward; the root's record is GpuScene::root_w)        48 B
 //   geoms  GpuGeom per geometry (material of CUTracer.cu:300-308)      64 B
 // Shading normals live outside the image (read once per shaded hit):
 //   normals 3 x float4 per KD triangle (n0, n1, n2)                    48 B
@@ -40,7 +40,7 @@ struct GpuScene {
     const float4* normals;
     uint32_t image_bytes;
     uint32_t off_tris, off_nodes, off_leafs, off_geoms;
-    uint32_t off_lboxes, leaf_boxes;     // leaf box records (global-memory scenes): fp16 box + count
+    uint32_t node_boxes;                 // 1: 48-B pair records with child boxes (global-memory scenes)
     uint32_t n_tris, n_nodes, n_leafs, n_geoms;
     float root_min[3], root_max[3];
     uint32_t root_w[2];                  // root node record (nodes[0])

@@ -158,11 +158,13 @@ __device__ __forceinline__ void test_tri(RayState& r, const float4* __restrict__
 #endif
 constexpr int kDescentCap = MCPT_DESCENT_CAP;
 constexpr uint32_t kTriCap = MCPT_TRI_CAP;
-// Leaf box cull (scenes in global memory): the leaf's KD box, stored as fp16
-// rounded outward (half_box.hpp), against the ray segment (0, best].  A hit
-// at t in (0, best] lies inside the exact box, hence inside the stored one,
-// and its slabs contain t up to rounding, which the 2^-12 margins cover: the
-// cull never drops a hit that could improve `best`.
+// Child-box cull (scenes in global memory): each sibling-pair record also
+// carries both children's KD boxes (the node region clipped to its
+// triangles' bounds, KDTree.hpp:154-155) as fp16 rounded outward
+// (half_box.hpp).  A child whose box the ray segment (0, best] misses is not
+// entered: a hit that could improve `best` lies inside the exact box, hence
+// inside the stored one, and its slab intervals contain t up to rounding,
+// which the 2^-12 margins cover.
 __device__ __forceinline__ float h2f(uint32_t bits16) {
     return (float)__builtin_bit_cast(_Float16, (unsigned short)bits16);
 }
@@ -177,20 +179,38 @@ __device__ __forceinline__ void box_slab(float o, float d, float inv, float blo,
         hi = a1 < hi ? a1 : hi;
     }
 }
-__device__ __forceinline__ bool leaf_box_hit(const RayState& r, uint4 rb) {
+// box = lo.x lo.y | lo.z hi.x | hi.y hi.z as three packed fp16 pairs
+__device__ __forceinline__ bool box_hit(const RayState& r, uint32_t b0, uint32_t b1, uint32_t b2) {
     float lo = 0.0f, hi = r.best;
     bool out = false;
-    box_slab(r.o.x, r.d.x, r.ix, h2f(rb.x & 0xFFFFu), h2f(rb.y >> 16), lo, hi, out);
-    box_slab(r.o.y, r.d.y, r.iy, h2f(rb.x >> 16), h2f(rb.z & 0xFFFFu), lo, hi, out);
-    box_slab(r.o.z, r.d.z, r.iz, h2f(rb.y & 0xFFFFu), h2f(rb.z >> 16), lo, hi, out);
+    box_slab(r.o.x, r.d.x, r.ix, h2f(b0 & 0xFFFFu), h2f(b1 >> 16), lo, hi, out);
+    box_slab(r.o.y, r.d.y, r.iy, h2f(b0 >> 16), h2f(b2 & 0xFFFFu), lo, hi, out);
+    box_slab(r.o.z, r.d.z, r.iz, h2f(b1 & 0xFFFFu), h2f(b2 >> 16), lo, hi, out);
     return !out && !(lo * kEpsLo > hi * kEpsHi);
+}
+
+// Pop the next interval: false = traversal finished (empty stack, or the best
+// hit lies before the popped interval)
+template <int S>
+__device__ __forceinline__ bool pop_entry(RayState& r, uint4* st, int stride, uint4* __restrict__ spill,
+                                          uint32_t spill_stride) {
+    if (r.sp == 0) return false;
+    r.sp--;
+    uint4* slot = st + (r.sp & (S - 1)) * stride;
+    const uint4 e = *slot;
+    r.nw0 = e.x;
+    r.nw1 = e.y;
+    r.tmin = __uint_as_float(e.z);
+    r.tmax = __uint_as_float(e.w);
+    if (r.sp >= S) *slot = spill[(uint32_t)(r.sp - S) * spill_stride];
+    return !(r.best <= r.tmin * kEpsLo);
 }
 
 template <int S, bool BOXES = false>
 __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict__ tris,
                                           const uint2* __restrict__ nodes1, const uint32_t* __restrict__ leafs,
                                           uint4* st, int stride, uint4* __restrict__ spill, uint32_t spill_stride,
-                                          Counters& c MCPT_LU_PARAM, const uint4* __restrict__ lboxes = nullptr) {
+                                          Counters& c MCPT_LU_PARAM, const uint4* __restrict__ pairs = nullptr) {
     if (r.lpos == r.lend) {                   // between leaves: descend
         uint32_t w0 = r.nw0, w1 = r.nw1;
         int steps = 0;
@@ -204,7 +224,15 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
             c.inner++;
             MCPT_LANE_USE(desc_w, desc_l, lu);
             const uint32_t left = w0 & 0x3FFFFFFFu;
-            const uint4 pr = *reinterpret_cast<const uint4*>(nodes1 + left);   // children left, left+1
+            uint4 pr, bx0, bx1;
+            if constexpr (BOXES) {            // 48-B pair record: words, box(left), box(right)
+                const uint4* rec = pairs + 3u * ((left - 1u) >> 1);
+                pr = rec[0];
+                bx0 = rec[1];
+                bx1 = rec[2];
+            } else {
+                pr = *reinterpret_cast<const uint4*>(nodes1 + left);   // children left, left+1
+            }
             const int a = (int)(w0 >> 30);
             const float sv = __uint_as_float(w1);
             const float oa = sel3(a, r.o.x, r.o.y, r.o.z);
@@ -217,7 +245,16 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
             const bool no = !(t > 0.0f) | (t > r.tmax * kEpsHi);        // near child only
             const bool fo = t * kEpsHi < r.tmin;                        // far child only
             const bool go_far = !pp & !no & fo;
-            const bool push_it = pp | (!no & !fo);
+            const bool both = !pp & !no & !fo;                          // push far, go near
+            bool push_it = pp | both;
+            bool near_ok = true, far_ok = true;
+            if constexpr (BOXES) {
+                const bool hl = box_hit(r, bx0.x, bx0.y, bx0.z);
+                const bool hr = box_hit(r, bx0.w, bx1.x, bx1.y);
+                near_ok = below ? hl : hr;
+                far_ok = below ? hr : hl;
+                push_it = push_it & far_ok;
+            }
             const uint32_t n0 = below ? pr.x : pr.z, n1 = below ? pr.y : pr.w;     // near child record
             const uint32_t f0 = below ? pr.z : pr.x, f1 = below ? pr.w : pr.y;     // far child record
             if (push_it) {
@@ -229,19 +266,24 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
                 }
                 *slot = make_uint4(f0, f1, __float_as_uint(plo), __float_as_uint(r.tmax));
                 r.sp++;
-                if (!pp) r.tmax = t < r.tmax ? t : r.tmax;
+                if constexpr (!BOXES)                                   // here push_it & !pp == both
+                    if (!pp) r.tmax = t < r.tmax ? t : r.tmax;
             }
+            if constexpr (BOXES)                                        // the near child's interval,
+                if (both) r.tmax = t < r.tmax ? t : r.tmax;             // pushed far or not
             w0 = go_far ? f0 : n0;
             w1 = go_far ? f1 : n1;
+            if constexpr (BOXES) {
+                if (!(go_far ? far_ok : near_ok)) {   // the chosen child's box is missed: next interval
+                    if (!pop_entry<S>(r, st, stride, spill, spill_stride)) return true;
+                    w0 = r.nw0;
+                    w1 = r.nw1;
+                }
+            }
         }
         c.leaf++;
         r.lpos = w0 & 0x3FFFFFFFu;
-        uint32_t cnt = w1;
-        if constexpr (BOXES) {                // y word = leaf ordinal; count in the box record
-            const uint4 rb = lboxes[w1];
-            cnt = leaf_box_hit(r, rb) ? rb.w : 0u;
-        }
-        r.lend = r.lpos + cnt;
+        r.lend = r.lpos + w1;
     }
     for (uint32_t i = 0; i < kTriCap && r.lpos < r.lend; i++, r.lpos++) {
         c.refs++;
@@ -250,16 +292,7 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
         test_tri(r, tris, leafs[r.lpos]);
     }
     if (r.lpos < r.lend) return false;        // more triangles in this leaf
-    if (r.sp == 0) return true;
-    r.sp--;
-    uint4* slot = st + (r.sp & (S - 1)) * stride;
-    const uint4 e = *slot;
-    r.nw0 = e.x;
-    r.nw1 = e.y;
-    r.tmin = __uint_as_float(e.z);
-    r.tmax = __uint_as_float(e.w);
-    if (r.sp >= S) *slot = spill[(uint32_t)(r.sp - S) * spill_stride];
-    return r.best <= r.tmin * kEpsLo;
+    return !pop_entry<S>(r, st, stride, spill, spill_stride);
 }
 
 // work unit v (packed owned-pixel index) -> image pixel; false outside the image

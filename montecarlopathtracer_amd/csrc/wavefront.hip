@@ -181,7 +181,7 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
         leafs = reinterpret_cast<const uint32_t*>(sc.image + sc.off_leafs);
         geoms = reinterpret_cast<const GpuGeom*>(sc.image + sc.off_geoms);
     }
-    const uint4* lboxes = reinterpret_cast<const uint4*>(sc.image + sc.off_lboxes);   // global variant only
+    const uint4* pairs = reinterpret_cast<const uint4*>(sc.image + sc.off_nodes);   // 48-B pair records (global variant)
     __syncthreads();
     uint4* st = reinterpret_cast<uint4*>(smem + kp.lds_stack_off) + tid;
     uint4* spill = kp.spill + (blockIdx.x * BLOCK + (uint32_t)tid);
@@ -223,7 +223,7 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
         // ---- traversal burst until enough lanes are done ---------------------
         for (;;) {
             if (mode == kTrav) {
-                if (trav_iter<S, !IN_LDS>(r, tris, nodes, leafs, st, BLOCK, spill, spill_stride, c MCPT_LU_ARG, lboxes)) mode = kReady;
+                if (trav_iter<S, !IN_LDS>(r, tris, nodes, leafs, st, BLOCK, spill, spill_stride, c MCPT_LU_ARG, pairs)) mode = kReady;
             }
             const uint64_t trv = __ballot(mode == kTrav);
             const uint64_t rdy = __ballot(mode == kReady);

@@ -68,8 +68,8 @@ typedef struct {
                                        0: no tint (rtx.hlsl:345, the published renders) */
     int32_t mode;                   /* 0: CVMCTracer semantics; 1: QuinEngine (rtx.hlsl:304-405) */
     float proj11, proj22;           /* QE: PerspectiveFovRH scales (orc_qe_proj)  */
-    int32_t leaf_boxes;             /* ordered KD: cull leaves by their fp16 KD box (the
-                                       kernel does for scenes served from global memory) */
+    int32_t node_boxes;             /* ordered KD: skip children whose fp16 KD box the ray
+                                       misses (the kernel does for scenes in global memory) */
 } orc_params;
 
 typedef struct {

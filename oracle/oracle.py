@@ -28,7 +28,7 @@ class Params(C.Structure):
         ("eye", C.c_float * 3), ("fwd", C.c_float * 3), ("up", C.c_float * 3), ("right", C.c_float * 3),
         ("seed", C.c_uint64), ("traversal", C.c_int32), ("threads", C.c_int32),
         ("prev_count", C.c_uint32), ("fresnel_kd", C.c_int32),
-        ("mode", C.c_int32), ("proj11", C.c_float), ("proj22", C.c_float), ("leaf_boxes", C.c_int32),
+        ("mode", C.c_int32), ("proj11", C.c_float), ("proj22", C.c_float), ("node_boxes", C.c_int32),
     ]
 
 
@@ -201,7 +201,7 @@ class RenderParams:
     def __init__(self, width=64, height=64, spp=4, spp_offset=0, spp_chunk=0, max_depth=7, illum=10.0,
                  fov=60.0, scene_id=1, eye=None, direction=(0, 0, -1), up=(0, 1, 0), seed=0x4D435054,
                  traversal=KD_ORDERED, threads=1, region=None, prev_count=0, fresnel_kd=1, mode=MODE_CV,
-                 leaf_boxes=0):
+                 node_boxes=0):
         self.width, self.height, self.spp, self.spp_offset, self.spp_chunk = width, height, spp, spp_offset, spp_chunk
         self.max_depth, self.illum, self.fov, self.seed = max_depth, illum, fov, seed
         if eye is None:
@@ -210,7 +210,7 @@ class RenderParams:
         self.traversal, self.threads, self.prev_count, self.fresnel_kd = traversal, threads, prev_count, fresnel_kd
         self.region = region or (0, 0, width, height)
         self.mode = mode
-        self.leaf_boxes = leaf_boxes
+        self.node_boxes = node_boxes
 
     def to_c(self):
         P = Params()
@@ -225,7 +225,7 @@ class RenderParams:
         P.seed = self.seed
         P.traversal, P.threads, P.prev_count, P.fresnel_kd = self.traversal, self.threads, self.prev_count, self.fresnel_kd
         P.mode = self.mode
-        P.leaf_boxes = self.leaf_boxes
+        P.node_boxes = self.node_boxes
         if self.mode == MODE_QE:
             p11, p22 = C.c_float(), C.c_float()
             lib().orc_qe_proj(C.c_float(self.fov), self.width, self.height, C.byref(p11), C.byref(p22))

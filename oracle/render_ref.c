@@ -294,7 +294,7 @@ typedef struct {
     const orc_scene* s;
     const orc_v3 (*kv)[3];   /* vertices by kd id */
     int traversal;
-    int leaf_boxes;          /* ordered walk: fp16 leaf-box cull */
+    int node_boxes;          /* ordered walk: fp16 child-box cull */
     float best_init;         /* FLT_MAX (CUTracer.cu:46); 10000 in QE mode (rtx.hlsl:88) */
     orc_counters c;
 } qctx;
@@ -437,8 +437,8 @@ uint16_t orc_f16_dir(float x, int dir) {
     if (mag == 0 && sg) return (uint16_t)0x8000u;
     return (uint16_t)((sg << 15) | mag);
 }
-/* does the ray segment (0, best] meet the leaf's fp16 box?  (trace_device.hpp leaf_box_hit) */
-static int leaf_box_hit(const orc_node* nd, const float* oo, const float* dd, const float* inv, float best) {
+/* does the ray segment (0, best] meet the node's fp16 box?  (trace_device.hpp box_hit) */
+static int box_hit(const orc_node* nd, const float* oo, const float* dd, const float* inv, float best) {
     float lo = 0.0f, hi = best;
     int out = 0;
     for (int a = 0; a < 3; a++) {
@@ -494,25 +494,35 @@ static hit_t isect_kd_ordered(qctx* q, orc_v3 o, orc_v3 d) {
             int below = (oo[a] < sv) || (oo[a] == sv && dd[a] <= 0.0f);
             uint32_t nearc = below ? nd->left : nd->right;
             uint32_t farc = below ? nd->right : nd->left;
+            /* child-box cull (scenes the kernel serves from global memory) */
+            int nhit = 1, fhit = 1;
+            if (q->node_boxes) {
+                nhit = box_hit(&s->nodes[nearc], oo, dd, inv, best);
+                fhit = box_hit(&s->nodes[farc], oo, dd, inv, best);
+            }
             if (dd[a] == 0.0f && oo[a] == sv) {
-                st_node[sp] = farc; st_lo[sp] = tmin; st_hi[sp] = tmax; sp++;
+                if (fhit) { st_node[sp] = farc; st_lo[sp] = tmin; st_hi[sp] = tmax; sp++; }
                 node = nearc;
             } else if (!(t > 0.0f) || t > tmax * KD_EPS_HI) {
                 node = nearc;
             } else if (t * KD_EPS_HI < tmin) {
                 node = farc;
             } else {
-                st_node[sp] = farc; st_lo[sp] = t > tmin ? t : tmin; st_hi[sp] = tmax; sp++;
+                if (fhit) { st_node[sp] = farc; st_lo[sp] = t > tmin ? t : tmin; st_hi[sp] = tmax; sp++; }
                 node = nearc;
                 tmax = t < tmax ? t : tmax;
+            }
+            if (!(node == nearc ? nhit : fhit)) {   /* chosen child missed: next interval */
+                if (sp == 0) return h;
+                sp--;
+                node = st_node[sp]; tmin = st_lo[sp]; tmax = st_hi[sp];
+                if (best <= tmin * KD_EPS_LO) return h;
             }
             if ((uint64_t)sp > q->c.stack_max) q->c.stack_max = (uint64_t)sp;
             nd = &s->nodes[node];
         }
         q->c.leaf_visits++;
-        uint32_t cnt = nd->tri_count;
-        if (q->leaf_boxes && !leaf_box_hit(nd, oo, dd, inv, best)) cnt = 0;
-        for (uint32_t i = 0; i < cnt; i++) {
+        for (uint32_t i = 0; i < nd->tri_count; i++) {
             uint32_t k = s->leaf_ids[nd->tri_begin + i];
             q->c.leaf_refs++;
             q->c.tri_tests++;
@@ -776,7 +786,7 @@ static void* render_worker(void* arg) {
     q.s = j->s;
     q.kv = j->kv;
     q.traversal = p->traversal;
-    q.leaf_boxes = p->leaf_boxes;
+    q.node_boxes = p->node_boxes;
     q.best_init = p->mode == 1 ? QE_T_BEST : FLT_MAX;
     uint32_t key = orc_seed_key(p->seed);
     for (;;) {

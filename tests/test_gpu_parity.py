@@ -24,17 +24,17 @@ CASES = [
 ]
 
 
-def _leaf_boxes(mcpt, scene_path):
-    """The kernel culls leaves by their fp16 boxes for scenes served from global memory."""
-    return int(mcpt.Scene(mcpt.ObjModel(scene_path), host_only=True).info()["leaf_boxes"])
+def _node_boxes(mcpt, scene_path):
+    """The kernel culls children by their fp16 KD boxes for scenes served from global memory."""
+    return int(mcpt.Scene(mcpt.ObjModel(scene_path), host_only=True).info()["node_boxes"])
 
 
 def _oracle_render(oracle_mod, scene_path, W, H, spp, chunk, depth, seed, fkd, illum, scene_id, offset=0, prev=None,
-                   prev_count=0, leaf_boxes=0):
+                   prev_count=0, node_boxes=0):
     o = oracle_mod.Scene(scene_path)
     p = oracle_mod.RenderParams(width=W, height=H, spp=spp, spp_chunk=chunk, max_depth=depth, seed=seed,
                                 fresnel_kd=fkd, illum=illum, scene_id=scene_id, traversal=oracle_mod.KD_ORDERED,
-                                threads=8, spp_offset=offset, prev_count=prev_count, leaf_boxes=leaf_boxes)
+                                threads=8, spp_offset=offset, prev_count=prev_count, node_boxes=node_boxes)
     out = None if prev is None else prev.copy()
     return o.render(p, out)
 
@@ -46,7 +46,7 @@ def test_image_and_counters_match_oracle(mcpt, oracle_mod, case, pipeline):
     path = mcpt.scene_path(sc)
     scene_id = 2 if sc in ("scene02", "scene03") else 1
     ref, rc = _oracle_render(oracle_mod, path, W, H, spp, chunk, depth, seed, fkd, illum, scene_id,
-                             leaf_boxes=_leaf_boxes(mcpt, path))
+                             node_boxes=_node_boxes(mcpt, path))
     scene = mcpt.Scene(mcpt.ObjModel(path))
     p = mcpt.RenderParams.for_scene(scene_id, width=W, height=H, spp=spp, spp_chunk=chunk, max_depth=depth,
                                     seed=seed, fresnel_kd=bool(fkd), illum=illum, pipeline=pipeline)
@@ -164,7 +164,7 @@ def test_quinengine_mode_matches_oracle(mcpt, oracle_mod, case, pipeline):
     o = oracle_mod.Scene(path)
     ref, rc = o.render(oracle_mod.RenderParams(width=W, height=H, spp=spp, spp_chunk=chunk, max_depth=depth,
                                                seed=seed, illum=1.0, fov=45.0, fresnel_kd=0, threads=8,
-                                               mode=oracle_mod.MODE_QE, leaf_boxes=_leaf_boxes(mcpt, path)))
+                                               mode=oracle_mod.MODE_QE, node_boxes=_node_boxes(mcpt, path)))
     scene = mcpt.Scene(mcpt.ObjModel(path))
     img, st = scene.render(_qe_params(mcpt, W, H, spp, chunk, depth, seed, pipeline=pipeline))
     assert np.array_equal(img, ref), f"max abs diff {np.abs(img - ref).max()}"

@@ -198,18 +198,19 @@ def test_quinengine_mode_brute_equals_kd_and_is_gamma_encoded(oracle_mod, mcpt):
     assert cc["rays"] <= 4 * cc["paths"]
 
 
-def test_leaf_box_cull_is_exact_and_prunes(oracle_mod, mcpt):
-    """The fp16 leaf-box cull the kernel applies to scenes in global memory:
-    identical images with it on and off; most triangle tests disappear."""
+def test_child_box_cull_is_exact_and_prunes(oracle_mod, mcpt):
+    """The fp16 child-box cull the kernel applies to scenes in global memory:
+    identical images with it on and off; most node visits and triangle tests disappear."""
     for name, sid in (("scene01", 1), ("scene02", 2), ("scene03", 2)):
         s = oracle_mod.Scene(mcpt.scene_path(name))
         kw = dict(width=40, height=30, spp=3, threads=8, scene_id=sid, traversal=oracle_mod.KD_ORDERED)
-        a, ca = s.render(oracle_mod.RenderParams(leaf_boxes=0, **kw))
-        b, cb = s.render(oracle_mod.RenderParams(leaf_boxes=1, **kw))
+        a, ca = s.render(oracle_mod.RenderParams(node_boxes=0, **kw))
+        b, cb = s.render(oracle_mod.RenderParams(node_boxes=1, **kw))
         assert np.array_equal(a, b), name
-        assert ca["rays"] == cb["rays"] and ca["inner_visits"] == cb["inner_visits"]
-        assert cb["tri_tests"] <= ca["tri_tests"]
+        assert ca["rays"] == cb["rays"] and ca["shades"] == cb["shades"]
+        assert cb["inner_visits"] <= ca["inner_visits"] and cb["tri_tests"] <= ca["tri_tests"]
         if name != "scene03":   # scene03 from camera 2: few leaves, all of them hit
+            assert cb["inner_visits"] < 0.8 * ca["inner_visits"], (name, ca["inner_visits"], cb["inner_visits"])
             assert cb["tri_tests"] < 0.5 * ca["tri_tests"], (name, ca["tri_tests"], cb["tri_tests"])
 
 
