@@ -167,6 +167,15 @@ int mcpt_model_group(const mcpt_model* m, int64_t g, char* name_buf, int64_t nam
 int mcpt_scene_create(const mcpt_model* m, mcpt_scene** out);
 /* Same, but host-only: no device allocation (KD inspection / CPU tests).   */
 int mcpt_scene_create_host(const mcpt_model* m, mcpt_scene** out);
+/* Same as mcpt_scene_create (host_only = 0) / _create_host (host_only = 1),
+ * with an on-disk KD-build cache in kd_cache_dir (must exist; NULL or "" =
+ * no cache).  The tree is a pure function of the triangle vertices, keyed by
+ * two 64-bit hashes of them; a file that fails any check is rebuilt and
+ * rewritten.  *cache_hit (may be NULL) = 1 if the tree was read, 0 if built.
+ * (the reference rebuilds its tree on every start,
+ * QuinEngine/RTX/ShaderResource.hpp:128-179.)                              */
+int mcpt_scene_create_cached(const mcpt_model* m, const char* kd_cache_dir, int32_t host_only,
+                             mcpt_scene** out, int32_t* cache_hit);
 void mcpt_scene_destroy(mcpt_scene* s);
 int mcpt_scene_get_info(const mcpt_scene* s, mcpt_scene_info* out);
 /* KD tree as built (BFS order, QuinEngine/RTX/ShaderResource.hpp:128-179):

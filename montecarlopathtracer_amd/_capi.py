@@ -100,6 +100,7 @@ _SIGS = {
     "mcpt_model_group": (C.c_int, [_vp, C.c_int64, C.c_char_p, C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_int32)]),
     "mcpt_scene_create": (C.c_int, [_vp, C.POINTER(_vp)]),
     "mcpt_scene_create_host": (C.c_int, [_vp, C.POINTER(_vp)]),
+    "mcpt_scene_create_cached": (C.c_int, [_vp, C.c_char_p, C.c_int32, C.POINTER(_vp), C.POINTER(C.c_int32)]),
     "mcpt_scene_destroy": (None, [_vp]),
     "mcpt_scene_get_info": (C.c_int, [_vp, C.POINTER(SceneInfo)]),
     "mcpt_scene_copy_kd": (C.c_int, [_vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_int32),

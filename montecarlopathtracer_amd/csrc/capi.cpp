@@ -125,14 +125,15 @@ struct mcpt_scene {
 
 namespace {
 
-// Device node order: 128-B "treelet" clusters.  A cluster holds the sibling
-// pairs of the 3 levels below its root (<= 7 pairs = 112 B) and never
-// straddles a 128-B line, so one line serves 3 levels of a descent; clusters
-// are emitted breadth-first (the top of the tree comes first).  Slot 0 is
-// padding and slot 1 the root, so the root's own cluster fills line 0.
-// Triangles and leaf references are renumbered in the order the leaves
-// appear, so a leaf's triangles sit near its neighbours'.  Only addresses
-// change: traversal order, results and counters are those of the BFS tree.
+// Device node order: treelet clusters.  A cluster holds the sibling pairs of
+// the 3 levels below its root (<= 7 pairs) contiguously, so a descent through
+// those levels stays within 112 B (16-B pairs, LDS scenes) or 336 B (48-B
+// pair records with child boxes, global-memory scenes); clusters are emitted
+// breadth-first (the top of the tree comes first).  Slot 0 is padding and
+// slot 1 the root.  Triangles and leaf references are renumbered in the order
+// the leaves appear, so a leaf's triangles sit near its neighbours'.  Only
+// addresses change: traversal order, results and counters are those of the
+// BFS tree.
 struct DeviceOrder {
     std::vector<uint32_t> node_new;     // host node -> device node index
     uint32_t n_slots = 0;               // device node indices in use (incl. padding)
@@ -141,7 +142,7 @@ struct DeviceOrder {
     std::vector<uint32_t> tri_new;      // kd id -> device triangle slot
 };
 
-DeviceOrder device_order(const mcpt::HostScene& hs, bool align_lines) {
+DeviceOrder device_order(const mcpt::HostScene& hs) {
     const uint32_t nn = static_cast<uint32_t>(hs.nodes.size());
     DeviceOrder d;
     d.node_new.assign(nn, 0xFFFFFFFFu);
@@ -164,8 +165,6 @@ DeviceOrder device_order(const mcpt::HostScene& hs, bool align_lines) {
         for (uint32_t n : frontier)
             if (hs.nodes[n].axis) queue.push_back(n);
         if (list.empty()) continue;
-        const uint32_t used = (pairs + 1) % 8;                  // pairs already in the current line
-        if (align_lines && used && used + list.size() > 8) pairs += 8 - used;  // start a fresh line
         for (uint32_t L : list) {
             d.node_new[L] = 2 * pairs + 1;
             d.node_new[L + 1] = 2 * pairs + 2;
@@ -212,7 +211,7 @@ void build_image(mcpt_scene& s) {
     // LDS byte counts).  Larger scenes: 48-B sibling-pair records -- the two
     // node words plus both children's KD boxes as fp16 rounded outward, so the
     // traversal skips children the ray misses (child-box cull).
-    DeviceOrder ord = device_order(hs, false);
+    DeviceOrder ord = device_order(hs);
     bool boxes = false;
     auto image_size = [&](const DeviceOrder& o, size_t& on, size_t& ol, size_t& og) {
         on = al128(size_t(nt) * 48);
@@ -706,11 +705,14 @@ int mcpt_model_group(const mcpt_model* m, int64_t g, char* name_buf, int64_t nam
     return MCPT_OK;
 }
 
-static int scene_create_impl(const mcpt_model* m, mcpt_scene** out, bool device) {
+static int scene_create_impl(const mcpt_model* m, mcpt_scene** out, bool device, const char* kd_cache_dir = nullptr,
+                             int32_t* cache_hit = nullptr) {
     return guarded([&]() -> int {
         if (!m || !out) return fail(MCPT_E_INVALID, "NULL argument");
         auto s = std::make_unique<mcpt_scene>();
-        mcpt::build_host_scene(m->m, s->hs);
+        int hit = 0;
+        mcpt::build_host_scene(m->m, s->hs, kd_cache_dir, &hit);
+        if (cache_hit) *cache_hit = hit;
         if (s->hs.kd_tris.empty()) return fail(MCPT_E_INVALID, "scene has no triangles");
         build_image(*s);
         if (device) {
@@ -737,6 +739,10 @@ static int scene_create_impl(const mcpt_model* m, mcpt_scene** out, bool device)
 
 int mcpt_scene_create(const mcpt_model* m, mcpt_scene** out) { return scene_create_impl(m, out, true); }
 int mcpt_scene_create_host(const mcpt_model* m, mcpt_scene** out) { return scene_create_impl(m, out, false); }
+int mcpt_scene_create_cached(const mcpt_model* m, const char* kd_cache_dir, int32_t host_only, mcpt_scene** out,
+                             int32_t* cache_hit) {
+    return scene_create_impl(m, out, host_only == 0, kd_cache_dir, cache_hit);
+}
 
 void mcpt_scene_destroy(mcpt_scene* s) { delete s; }
 

@@ -224,7 +224,7 @@ void read_obj(const std::string& path, ObjModel& m) {   // ObjReader.cpp:8-161
 }
 
 // ---------------------------------------------------------------------------
-void build_host_scene(const ObjModel& m, HostScene& hs) {
+void build_host_scene(const ObjModel& m, HostScene& hs, const char* kd_cache_dir, int* cache_hit) {
     hs = HostScene();
     const int64_t ntri = static_cast<int64_t>(m.triangles.size());
     // CreateGeometry (CUTracer.cu:277-311): one record per non-empty group,
@@ -275,6 +275,16 @@ void build_host_scene(const ObjModel& m, HostScene& hs) {
             hs.kd_verts.insert(hs.kd_verts.end(), {p.x, p.y, p.z});
             hs.kd_normals.insert(hs.kd_normals.end(), {q.x, q.y, q.z});
         }
+    }
+    if (cache_hit) *cache_hit = 0;
+    if (kd_cache_dir && *kd_cache_dir) {
+        if (kd_cache_load(kd_cache_dir, hs.kd_verts, hs.nodes, hs.leaf_ids, hs.kd_depth)) {
+            if (cache_hit) *cache_hit = 1;
+            return;
+        }
+        build_kdtree(hs.kd_verts, hs.nodes, hs.leaf_ids, hs.kd_depth);
+        kd_cache_store(kd_cache_dir, hs.kd_verts, hs.nodes, hs.leaf_ids, hs.kd_depth);   // best effort
+        return;
     }
     build_kdtree(hs.kd_verts, hs.nodes, hs.leaf_ids, hs.kd_depth);
 }

@@ -70,8 +70,16 @@ struct HostScene {
     int kd_depth = 0;
 };
 
-// CreateGeometry semantics + KD build; throws mcpt::Error.
-void build_host_scene(const ObjModel& m, HostScene& out);
+// CreateGeometry semantics + KD build; throws mcpt::Error.  With a cache
+// directory the KD tree is read from / written to it (kd_cache.cpp);
+// *cache_hit (if given) = 1 when it was read, 0 when built.
+void build_host_scene(const ObjModel& m, HostScene& out, const char* kd_cache_dir = nullptr,
+                      int* cache_hit = nullptr);
+// on-disk KD cache (kd_cache.cpp): load returns false unless a valid file exists
+bool kd_cache_load(const std::string& dir, const std::vector<float>& tri_verts, std::vector<KdNode>& nodes,
+                   std::vector<uint32_t>& leaf_ids, int& depth);
+bool kd_cache_store(const std::string& dir, const std::vector<float>& tri_verts, const std::vector<KdNode>& nodes,
+                    const std::vector<uint32_t>& leaf_ids, int depth);
 // KD build only (KDTree.hpp semantics) over kd_verts; fills nodes/leaf_ids/kd_depth.
 void build_kdtree(const std::vector<float>& tri_verts, std::vector<KdNode>& nodes,
                   std::vector<uint32_t>& leaf_ids, int& depth);

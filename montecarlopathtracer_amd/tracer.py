@@ -19,6 +19,7 @@ Same names, argument meaning and call order.  Differences:
 from __future__ import annotations
 
 import ctypes as C
+import os
 from dataclasses import dataclass, field
 from typing import Optional, Sequence
 
@@ -227,10 +228,20 @@ class RenderParams:
 class Scene:
     """A device-resident scene (CreateGeometry result + KD tree)."""
 
-    def __init__(self, model: ObjModel, host_only: bool = False):
+    def __init__(self, model: ObjModel, host_only: bool = False, kd_cache: Optional[str] = None):
+        """kd_cache: directory for the on-disk KD-build cache (mcpt_scene_create_cached);
+        ``cache_hit`` tells whether the tree was read from it."""
         h = C.c_void_p()
-        fn = lib().mcpt_scene_create_host if host_only else lib().mcpt_scene_create
-        check(fn(model.handle, C.byref(h)))
+        self.cache_hit = False
+        if kd_cache:
+            os.makedirs(kd_cache, exist_ok=True)
+            hit = C.c_int32(0)
+            check(lib().mcpt_scene_create_cached(model.handle, os.fsencode(kd_cache), int(host_only),
+                                                 C.byref(h), C.byref(hit)))
+            self.cache_hit = bool(hit.value)
+        else:
+            fn = lib().mcpt_scene_create_host if host_only else lib().mcpt_scene_create
+            check(fn(model.handle, C.byref(h)))
         self._h = h
         self.host_only = host_only
 

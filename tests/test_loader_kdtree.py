@@ -198,3 +198,39 @@ def test_in_memory_model_rejects_bad_indices(mcpt):
         mcpt.ObjModel.from_arrays(v, n, t, mats, {"g": [5]})
     m = mcpt.ObjModel.from_arrays(v, n, t, mats, {"g": [1]})
     assert m.info()["n_triangles"] == 2
+
+
+def test_kd_cache_roundtrip_and_rejects_bad_files(mcpt, tmp_path):
+    """mcpt_scene_create_cached: the first call builds and
+    writes the tree, the second reads it; a corrupted, truncated or foreign
+    file is rebuilt -- the tree (and so every render) is identical each time."""
+    model = mcpt.ObjModel(mcpt.scene_path("scene02"))
+    ref = mcpt.Scene(model, host_only=True).kd()
+    d = str(tmp_path / "kd")
+
+    def same(scene):
+        for a, b in zip(ref, scene.kd()):
+            assert np.array_equal(a, b)
+
+    s1 = mcpt.Scene(model, host_only=True, kd_cache=d)
+    assert not s1.cache_hit
+    same(s1)
+    files = os.listdir(d)
+    assert len(files) == 1 and files[0].startswith("mcpt-kd-") and files[0].endswith(".bin")
+    s2 = mcpt.Scene(model, host_only=True, kd_cache=d)
+    assert s2.cache_hit
+    same(s2)
+    path = os.path.join(d, files[0])
+    blob = bytearray(open(path, "rb").read())
+    for bad in (blob[:-4],                                          # truncated
+                blob[:100] + bytes([blob[100] ^ 1]) + blob[101:],   # payload bit flip
+                blob + b"\0"):                                      # trailing bytes
+        open(path, "wb").write(bytes(bad))
+        s = mcpt.Scene(model, host_only=True, kd_cache=d)
+        assert not s.cache_hit
+        same(s)
+        assert open(path, "rb").read() == bytes(blob)             # rewritten
+    # another scene gets its own file and its own tree
+    other = mcpt.Scene(mcpt.ObjModel(mcpt.scene_path("scene01")), host_only=True, kd_cache=d)
+    assert not other.cache_hit and len(os.listdir(d)) == 2
+    assert other.info()["n_nodes"] != s2.info()["n_nodes"]
