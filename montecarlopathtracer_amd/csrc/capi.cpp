@@ -394,9 +394,10 @@ Plan make_plan(const mcpt_scene& s, const mcpt_render_params* p) {
         throw mcpt::Error{MCPT_E_INVALID, "unknown pipeline"};
     pl.pipeline = p->pipeline;
     {
-        uint64_t cap = p->wf_batch ? p->wf_batch : (1u << 24);
+        uint64_t cap = p->wf_batch ? p->wf_batch : (1u << 25);          // C2: 2^24 4.82, 2^25 5.07, 2^26 5.05
         cap = std::max<uint64_t>(cap, chunk);                        // at least one pixel per batch
-        cap = std::min<uint64_t>(cap, std::max<uint64_t>(npix, 1) * chunk);
+        cap = std::min<uint64_t>(cap, std::max<uint64_t>(npix, 1) * std::max<uint64_t>(p->spp, chunk));
+        cap = std::min<uint64_t>(cap, uint64_t(1) << 27);               // u32 slot arithmetic, 17 GB of queues
         pl.wf_capacity = static_cast<uint32_t>(cap);
     }
     return pl;
@@ -425,17 +426,13 @@ mcpt::WfParams prepare_wavefront(mcpt_scene& s, const Plan& pl) {
     // segments hold whole path groups (<= 2^14): up to nseg groups of slots beyond the paths
     const size_t cap_slots = cap + size_t(mcpt::wavefront_segments(s.gpu.image_bytes, s.cus)) * 16384;
     const size_t f4 = cap_slots * 16;
-    const size_t need = 4 * f4 + f4 + 4 * cap_slots * 4 + 2 * f4 + bounces * sizeof(mcpt::WfCounters) + 256;
+    const size_t need = 2 * 4 * f4 + f4 + 4 * cap_slots * 4 + bounces * sizeof(mcpt::WfCounters) + 256;
     ensure_buf(s.ws.wf, s.ws.wf_bytes, need);
     char* b = static_cast<char*>(s.ws.wf);
     mcpt::WfParams w;
     std::memset(&w, 0, sizeof w);
-    w.q_o[0] = reinterpret_cast<float4*>(b); b += f4;
-    w.q_o[1] = reinterpret_cast<float4*>(b); b += f4;
-    w.q_d[0] = reinterpret_cast<float4*>(b); b += f4;
-    w.q_d[1] = reinterpret_cast<float4*>(b); b += f4;
-    w.hit = reinterpret_cast<float4*>(b); b += f4;
-    w.pstate = reinterpret_cast<float4*>(b); b += f4;
+    w.q[0] = reinterpret_cast<float4*>(b); b += 4 * f4;
+    w.q[1] = reinterpret_cast<float4*>(b); b += 4 * f4;
     w.radiance = reinterpret_cast<float4*>(b); b += f4;
     w.cls_list = reinterpret_cast<uint32_t*>(b); b += 4 * cap_slots * 4;
     w.cnt = reinterpret_cast<mcpt::WfCounters*>(b);

@@ -84,16 +84,17 @@ struct WfCounters {                      // per (bounce, segment), 8 words
     uint32_t pad[3];
 };
 struct WfParams {
-    float4* q_o[2];                      // ray origin .xyz, pid bits in .w          [capacity]
-    float4* q_d[2];                      // ray direction .xyz, depth bits in .w     [capacity]
-    float4* hit;                         // (t, beta, gamma, htri bits) per slot     [capacity]
+    // ray queue b: one 64-B record per slot, {o.xyz pid} {d.xyz depth}
+    // {t beta gamma htri} {throughput.xyz rng}: extend reads the first half
+    // and fills the hit, shade reads the whole record with one gather
+    float4* q[2];                        // [slot_stride][4]
     uint32_t* cls_list;                  // [4][capacity] slots per material class
-    float4* pstate;                      // (throughput .xyz, rng state bits) per pid [capacity]
     float4* radiance;                    // path radiance per pid                   [capacity]
     WfCounters* cnt;                     // [max_depth + 2][nseg]
     uint32_t capacity;                   // paths per batch
     uint32_t slot_stride;                // queue / class-list entries per array (>= nseg * seg)
-    uint32_t v0, nb, s_begin, ns, chunk_index;
+    uint32_t v0, nb, s_begin, ns, chunk_index;   // pixels [v0, v0+nb) x samples [s_begin, s_begin+ns)
+    uint32_t nsc;                        // samples per chunk (ns = whole chunks of nsc)
     uint32_t nseg, seg;                  // segments (= extend workgroups) and slots per segment
     uint32_t group_shift;                // paths are dealt to segments in groups of 2^group_shift
     int32_t bounce;

@@ -92,13 +92,13 @@ __global__ void __launch_bounds__(kGenBlock) wf_generate(const KernelParams kp, 
                 primary_ray_qe(kp, pix, px, py, wf.s_begin + s_local, sd, o, d);
             else
                 primary_ray(kp, pix, px, py, wf.s_begin + s_local, sd, d);
-            wf.pstate[pid] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(sd));
+            wf.q[0][4u * slot + 3u] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(sd));
             c.paths++;
             c.rays++;
             depth = 0;
         }
-        wf.q_o[0][slot] = pack(o, pid);
-        wf.q_d[0][slot] = pack(d, depth);
+        wf.q[0][4u * slot] = pack(o, pid);
+        wf.q[0][4u * slot + 1u] = pack(d, depth);
     }
     flush_counters(c, kp.stats);
 }
@@ -187,9 +187,7 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
     uint4* spill = kp.spill + (blockIdx.x * BLOCK + (uint32_t)tid);
     const uint32_t spill_stride = kp.total_lanes;
     const size_t seg0 = (size_t)g * wf.seg;
-    const float4* qo = wf.q_o[wf.bounce & 1] + seg0;
-    const float4* qd = wf.q_d[wf.bounce & 1] + seg0;
-    float4* hit = wf.hit + seg0;
+    float4* qr = wf.q[wf.bounce & 1] + 4u * seg0;          // this segment's records
 
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0};
 #ifdef MCPT_PHASE_TIMING
@@ -217,8 +215,8 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
             mode = begin_ray(r, sc, kp.best_init) ? kTrav : kReady;
         }
     };
-    if (slot < count) start(qo[slot], qd[slot]);
-    if (nslot < count) { no4 = qo[nslot]; nd4 = qd[nslot]; }
+    if (slot < count) start(qr[4u * slot], qr[4u * slot + 1u]);
+    if (nslot < count) { no4 = qr[4u * nslot]; nd4 = qr[4u * nslot + 1u]; }
     for (;;) {
         // ---- traversal burst until enough lanes are done ---------------------
         for (;;) {
@@ -233,7 +231,7 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
         const bool fin = mode == kReady;
         uint32_t cls = 4u;
         if (fin) {
-            hit[slot] = make_float4(r.best, r.hbeta, r.hgamma, __int_as_float(r.htri));
+            qr[4u * slot + 2u] = make_float4(r.best, r.hbeta, r.hgamma, __int_as_float(r.htri));
             cls = kClassTerminate;
             // CV: scatter while depth < max_depth (CUTracer.cu:103-160); QE: while
             // bounce < 3*depth (rtx.hlsl:312), roulette is drawn in shade
@@ -259,7 +257,7 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
         const uint32_t ns = cur_chunk.take(want, lcnt + 4);
         if (want) {
             nslot = ns;
-            if (nslot < count) { no4 = qo[nslot]; nd4 = qd[nslot]; }
+            if (nslot < count) { no4 = qr[4u * nslot]; nd4 = qr[4u * nslot + 1u]; }
         }
         if (!__ballot(mode != kDead)) break;
     }
@@ -284,11 +282,8 @@ __global__ void __launch_bounds__(kShadeBlock) wf_shade(const KernelParams kp, c
     const float4* tris = reinterpret_cast<const float4*>(sc.image + sc.off_tris);
     const GpuGeom* geoms = reinterpret_cast<const GpuGeom*>(sc.image + sc.off_geoms);
     const size_t seg0 = (size_t)g * wf.seg;
-    const float4* qo = wf.q_o[wf.bounce & 1] + seg0;
-    const float4* qd = wf.q_d[wf.bounce & 1] + seg0;
-    const float4* hit = wf.hit + seg0;
-    float4* qo2 = wf.q_o[(wf.bounce + 1) & 1] + seg0;
-    float4* qd2 = wf.q_d[(wf.bounce + 1) & 1] + seg0;
+    const float4* qr = wf.q[wf.bounce & 1] + 4u * seg0;
+    float4* qr2 = wf.q[(wf.bounce + 1) & 1] + 4u * seg0;
     const uint32_t p1 = cn->cls[1], p2 = p1 + cn->cls[2], p3 = p2 + cn->cls[3], total = p3 + cn->cls[0];
     if (q == 0 && threadIdx.x == 0) nx->queued = p3;
     const uint32_t lo = (uint32_t)(((uint64_t)total * q) / per), hi = (uint32_t)(((uint64_t)total * (q + 1)) / per);
@@ -297,7 +292,7 @@ __global__ void __launch_bounds__(kShadeBlock) wf_shade(const KernelParams kp, c
         const uint32_t k = i < p1 ? 1u : (i < p2 ? 2u : (i < p3 ? 3u : 0u));
         const uint32_t start = k == 1u ? 0u : (k == 2u ? p1 : (k == 3u ? p2 : p3));
         const uint32_t slot = wf.cls_list[(size_t)k * wf.slot_stride + seg0 + (i - start)];
-        const float4 o4 = qo[slot], d4 = qd[slot], h = hit[slot];
+        const float4 o4 = qr[4u * slot], d4 = qr[4u * slot + 1u], h = qr[4u * slot + 2u], ps = qr[4u * slot + 3u];
         const uint32_t pid = __float_as_uint(o4.w);
         const uint32_t depth = __float_as_uint(d4.w);
         const int32_t htri = __float_as_int(h.w);
@@ -310,33 +305,35 @@ __global__ void __launch_bounds__(kShadeBlock) wf_shade(const KernelParams kp, c
                 const GpuGeom& gm = geoms[__float_as_uint(tris[3 * htri + 1].w)];
                 if (qe) {
                     if ((int32_t)depth < 3 * kp.max_depth) {
-                        const float4 ps = wf.pstate[pid];
                         V3 color = xyz(ps);
                         uint32_t sd = __float_as_uint(ps.w);
                         if ((int32_t)depth < kp.max_depth || qe_roulette(sd, color)) L = emitted(color, gm, 1.0f);
                     }
                 } else if ((int32_t)depth >= kp.max_depth || is_emitter(gm)) {
-                    L = emitted(xyz(wf.pstate[pid]), gm, kp.illum);
+                    L = emitted(xyz(ps), gm, kp.illum);
                 }
             }
             wf.radiance[pid] = make_float4(L.x, L.y, L.z, 0.0f);
         } else {
-            const float4 ps = wf.pstate[pid];
             V3 color = xyz(ps);
             uint32_t sd = __float_as_uint(ps.w);
+            float4* nr = qr2 + 4u * i;                       // whole 64-B record written
             if (qe && (int32_t)depth >= kp.max_depth && !qe_roulette(sd, color)) {
                 // killed by the roulette: zero radiance, an empty slot in queue b+1
                 wf.radiance[pid] = make_float4(0, 0, 0, 0);
-                qo2[i] = pack(v3(0, 0, 0), pid);
-                qd2[i] = pack(v3(0, 0, 0), kNoRay);
+                nr[0] = pack(v3(0, 0, 0), pid);
+                nr[1] = pack(v3(0, 0, 0), kNoRay);
+                nr[2] = make_float4(0, 0, 0, 0);
+                nr[3] = make_float4(0, 0, 0, 0);
             } else {
                 c.shades++;
                 const GpuGeom& gm = geoms[__float_as_uint(tris[3 * htri + 1].w)];
                 V3 o = xyz(o4), d = xyz(d4);
                 scatter(gm, sc.normals, htri, h.y, h.z, h.x, qe ? 0 : kp.fresnel_kd, sd, color, o, d);
-                wf.pstate[pid] = pack(color, sd);
-                qo2[i] = pack(o, pid);
-                qd2[i] = pack(d, depth + 1u);
+                nr[0] = pack(o, pid);
+                nr[1] = pack(d, depth + 1u);
+                nr[2] = make_float4(0, 0, 0, 0);
+                nr[3] = pack(color, sd);
                 c.rays++;
             }
         }
@@ -345,12 +342,15 @@ __global__ void __launch_bounds__(kShadeBlock) wf_shade(const KernelParams kp, c
 }
 
 // ---- accumulate: samples of the batch in sample order -> partial sums -------
+// A batch holds wf.ns / wf.nsc whole chunks of nsc samples each (blockIdx.y).
 __global__ void __launch_bounds__(256) wf_accumulate(const KernelParams kp, const WfParams wf) {
     const uint32_t u = blockIdx.x * 256u + threadIdx.x;
     if (u >= wf.nb) return;
+    const uint32_t j = blockIdx.y;
     V3 part = v3(0, 0, 0);
-    for (uint32_t s = 0; s < wf.ns; s++) part = vadd(part, xyz(wf.radiance[(size_t)s * wf.nb + u]));
-    kp.partial[(size_t)wf.chunk_index * kp.npix_local + wf.v0 + u] = make_float4(part.x, part.y, part.z, 0.0f);
+    for (uint32_t s = j * wf.nsc; s < (j + 1u) * wf.nsc; s++)
+        part = vadd(part, xyz(wf.radiance[(size_t)s * wf.nb + u]));
+    kp.partial[(size_t)(wf.chunk_index + j) * kp.npix_local + wf.v0 + u] = make_float4(part.x, part.y, part.z, 0.0f);
 }
 
 template <bool IN_LDS, int S, int BLOCK>
@@ -392,12 +392,21 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams& wf_in, in
     const uint32_t per = in_lds ? 4u : 1u;                         // shade workgroups per segment
     hipError_t e = hipSuccess;
     if (ev0) hipEventRecord(ev0, st);
-    for (uint32_t chunk = 0; chunk < kp.nchunks; chunk++) {
+    for (uint32_t chunk = 0; chunk < kp.nchunks;) {
         WfParams wf = wf_in;
         wf.nseg = nseg;
         wf.chunk_index = chunk;
         wf.s_begin = chunk * kp.chunk;
-        wf.ns = (kp.spp - wf.s_begin) < kp.chunk ? (kp.spp - wf.s_begin) : kp.chunk;
+        wf.nsc = (kp.spp - wf.s_begin) < kp.chunk ? (kp.spp - wf.s_begin) : kp.chunk;
+        // whole-image batches may span several full chunks (fewer, longer launches)
+        uint32_t ncb = 1;
+        if (wf.nsc == kp.chunk && (uint64_t)kp.npix_local * kp.chunk <= wf.capacity) {
+            const uint32_t full = (kp.spp / kp.chunk) - chunk;             // full chunks left
+            const uint32_t fit = (uint32_t)(wf.capacity / ((uint64_t)kp.npix_local * kp.chunk));
+            ncb = fit < full ? fit : full;
+        }
+        wf.ns = ncb * wf.nsc;
+        chunk += ncb;
         const uint32_t nb_max = wf.capacity / wf.ns;
         for (uint32_t v0 = 0; v0 < kp.npix_local; v0 += nb_max) {
             wf.v0 = v0;
@@ -423,7 +432,7 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams& wf_in, in
                 hipLaunchKernelGGL(wf_shade, dim3(nseg * per), dim3(kShadeBlock), 0, st, kp, wf, per);
                 if ((e = hipGetLastError()) != hipSuccess) return e;
             }
-            hipLaunchKernelGGL(wf_accumulate, dim3((wf.nb + 255u) / 256u), dim3(256), 0, st, kp, wf);
+            hipLaunchKernelGGL(wf_accumulate, dim3((wf.nb + 255u) / 256u, ncb), dim3(256), 0, st, kp, wf);
             if ((e = hipGetLastError()) != hipSuccess) return e;
         }
     }
