@@ -503,8 +503,10 @@ void read_stats(mcpt_scene& s, mcpt_render_stats* out) {
                          "scatter %llu\n", st[8], st[9], st[10], st[11], st[12]);
 #ifdef MCPT_PHASE_TIMING
         {
-            unsigned long long lu[6];
+            unsigned long long lu[6], lw[6];
             mcpt::read_lane_use(lu);
+            mcpt::read_lane_use_wf(lw);
+            for (int i = 0; i < 6; i++) lu[i] += lw[i];
             std::fprintf(stderr, "mcpt lane use: descent %.3f (%llu wave-iters) triangle %.3f (%llu) burst %.3f (%llu)\n",
                          lu[0] ? double(lu[1]) / (64.0 * lu[0]) : 0.0, lu[0], lu[2] ? double(lu[3]) / (64.0 * lu[2]) : 0.0,
                          lu[2], lu[4] ? double(lu[5]) / (64.0 * lu[4]) : 0.0, lu[4]);

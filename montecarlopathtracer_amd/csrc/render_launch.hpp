@@ -108,7 +108,8 @@ hipError_t launch_render(const KernelParams& kp, int cus, hipStream_t st, hipEve
                          hipEvent_t ev2, float4* fb, int* variant_out);
 hipError_t launch_reduce(const KernelParams& kp, float4* fb, hipStream_t st);
 #ifdef MCPT_PHASE_TIMING
-void read_lane_use(unsigned long long out[6]);   // diagnostic build only
+void read_lane_use(unsigned long long out[6]);      // diagnostic build only: megakernel
+void read_lane_use_wf(unsigned long long out[6]);   // wavefront extend
 #endif
 // wavefront queue segments (= extend workgroups) for a scene image
 int wavefront_segments(uint32_t image_bytes, int cus);

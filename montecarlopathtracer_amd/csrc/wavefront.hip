@@ -60,6 +60,17 @@ __device__ __forceinline__ float opaque(float x) {
 __device__ __forceinline__ float4 pack(V3 v, uint32_t w) { return make_float4(v.x, v.y, v.z, __uint_as_float(w)); }
 __device__ __forceinline__ V3 xyz(float4 v) { return v3(v.x, v.y, v.z); }
 
+// Group k of block b (b-th run of nseg consecutive groups) -> its segment:
+// every block deals one group to each segment, rotated by a hash of b.  With
+// a plain k -> k (an image of 2^14 8x8 tiles, 256 segments) each segment got
+// the same 64 tiles for every sample -- a fixed stripe of the image, whose
+// cost differs from the others' and left CUs idle at the end of every extend.
+__device__ __forceinline__ uint32_t seg_of(uint32_t k, uint32_t b, uint32_t nseg) {
+    const uint32_t rot = (uint32_t)(((uint64_t)(b * 2654435761u) * nseg) >> 32);
+    const uint32_t g = k + rot;
+    return g >= nseg ? g - nseg : g;
+}
+
 // ---- generate: primary rays of the batch (CUTracer.cu:186-211) -------------
 // Paths go to segments in groups of 2^group_shift (64 = one 8x8 tile of one
 // sample: a coherent wave of primary rays), group j -> segment j % nseg, so
@@ -74,11 +85,16 @@ __global__ void __launch_bounds__(kGenBlock) wf_generate(const KernelParams kp, 
     for (uint32_t pid = blockIdx.x * kGenBlock + threadIdx.x; pid < n; pid += gridDim.x * kGenBlock) {
         const uint32_t s_local = pid / wf.nb;
         const uint32_t v = wf.v0 + (pid - s_local * wf.nb);
-        const uint32_t grp = pid >> gs, g = grp % wf.nseg;
-        const uint32_t slot = g * wf.seg + ((grp / wf.nseg) << gs) + (pid & gm);
-        if (grp < wf.nseg && (pid & gm) == 0u) {    // first path of segment g: its queue length
-            uint32_t len = ((ngroups - g + wf.nseg - 1u) / wf.nseg) << gs;
-            if ((ngroups - 1u) % wf.nseg == g) len -= (ngroups << gs) - n;
+        const uint32_t grp = pid >> gs, blk = grp / wf.nseg;
+        const uint32_t g = seg_of(grp - blk * wf.nseg, blk, wf.nseg);
+        const uint32_t slot = g * wf.seg + (blk << gs) + (pid & gm);
+        if (grp < wf.nseg && (pid & gm) == 0u) {    // segment g's queue length
+            const uint32_t full = ngroups / wf.nseg, rem = ngroups - full * wf.nseg;
+            // block `full` (partial, rem groups) covers segments rot, rot+1, ... (mod nseg)
+            const uint32_t k = (g + wf.nseg - seg_of(0, full, wf.nseg)) % wf.nseg;
+            uint32_t len = (full + (k < rem ? 1u : 0u)) << gs;
+            const uint32_t lb = (ngroups - 1u) / wf.nseg;            // block of the last group
+            if (seg_of(ngroups - 1u - lb * wf.nseg, lb, wf.nseg) == g) len -= (ngroups << gs) - n;
             wf.cnt[g].queued = len;
         }
         int px, py;
@@ -215,11 +231,26 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
             mode = begin_ray(r, sc, kp.best_init) ? kTrav : kReady;
         }
     };
+#ifdef MCPT_PHASE_TIMING
+    // stats[8] setup, [9] traversal bursts, [10] hand-offs, [11] burst iterations
+    unsigned long long tm_setup = 0, tm_trav = 0, tm_hand = 0, tm_iters = 0, tm_t0 = __builtin_amdgcn_s_memtime();
+#define WF_STAMP(acc) do { unsigned long long t1_ = __builtin_amdgcn_s_memtime(); acc += t1_ - tm_t0; tm_t0 = t1_; } while (0)
+#else
+#define WF_STAMP(acc) do {} while (0)
+#endif
     if (slot < count) start(qr[4u * slot], qr[4u * slot + 1u]);
     if (nslot < count) { no4 = qr[4u * nslot]; nd4 = qr[4u * nslot + 1u]; }
+    WF_STAMP(tm_setup);
     for (;;) {
         // ---- traversal burst until enough lanes are done ---------------------
         for (;;) {
+#ifdef MCPT_PHASE_TIMING
+            tm_iters++;
+            {
+                const uint64_t tv = __ballot(mode == kTrav);
+                if ((threadIdx.x & 63u) == 0) { lu.burst_w += 1; lu.burst_l += (unsigned long long)__popcll(tv); }
+            }
+#endif
             if (mode == kTrav) {
                 if (trav_iter<S, !IN_LDS>(r, tris, nodes, leafs, st, BLOCK, spill, spill_stride, c MCPT_LU_ARG, pairs)) mode = kReady;
             }
@@ -227,11 +258,19 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
             const uint64_t rdy = __ballot(mode == kReady);
             if (!trv || __popcll(rdy) >= wf.refill_thresh) break;
         }
+        WF_STAMP(tm_trav);
         // ---- hand-off: hit record + per-material class list -----------------
+        // Settle the prefetch (issued a whole burst ago) before any store of
+        // this hand-off: gfx9's vmcnt also counts stores, so any later wait on
+        // the prefetch registers would wait for the stores' acknowledgements.
+        no4 = make_float4(opaque(no4.x), opaque(no4.y), opaque(no4.z), no4.w);
+        nd4 = make_float4(opaque(nd4.x), opaque(nd4.y), opaque(nd4.z), opaque(nd4.w));
         const bool fin = mode == kReady;
         uint32_t cls = 4u;
+        const uint32_t fslot = slot;
+        float4 hrec = make_float4(0, 0, 0, 0);
         if (fin) {
-            qr[4u * slot + 2u] = make_float4(r.best, r.hbeta, r.hgamma, __int_as_float(r.htri));
+            hrec = make_float4(r.best, r.hbeta, r.hgamma, __int_as_float(r.htri));
             cls = kClassTerminate;
             // CV: scatter while depth < max_depth (CUTracer.cu:103-160); QE: while
             // bounce < 3*depth (rtx.hlsl:312), roulette is drawn in shade
@@ -240,29 +279,46 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
                 const GpuGeom& gm = geoms[__float_as_uint(tris[3 * r.htri + 1].w)];
                 if (!is_emitter(gm)) cls = material_class(gm);
             }
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < 4; k++)
-            out[k].append(cls == k, slot, lcnt + k, wf.cls_list + (size_t)k * wf.slot_stride + seg0);
-        // ---- finished lanes start their prefetched ray, prefetch another ------
-        if (fin) {
             if (nslot < count) {
                 slot = nslot;
                 start(no4, nd4);
             } else {
                 mode = kDead;
             }
+            qr[4u * fslot + 2u] = hrec;
         }
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++)
+            out[k].append(cls == k, fslot, lcnt + k, wf.cls_list + (size_t)k * wf.slot_stride + seg0);
+        // ---- prefetch the next ray of every lane that just started one -------
         const bool want = fin && mode != kDead;
         const uint32_t ns = cur_chunk.take(want, lcnt + 4);
         if (want) {
             nslot = ns;
             if (nslot < count) { no4 = qr[4u * nslot]; nd4 = qr[4u * nslot + 1u]; }
         }
+        WF_STAMP(tm_hand);
         if (!__ballot(mode != kDead)) break;
     }
 #pragma unroll
     for (uint32_t k = 0; k < 4; k++) out[k].flush(lcnt + k, wf.cls_list + (size_t)k * wf.slot_stride + seg0);
+#ifdef MCPT_PHASE_TIMING
+    if ((threadIdx.x & 63u) == 0) {
+        atomicAdd(kp.stats + 8, tm_setup);
+        atomicAdd(kp.stats + 9, tm_trav);
+        atomicAdd(kp.stats + 10, tm_hand);
+        atomicAdd(kp.stats + 11, tm_iters);
+    }
+    {
+        unsigned long long* gl = reinterpret_cast<unsigned long long*>(&g_lane_use);
+        const unsigned long long v[6] = {lu.desc_w, lu.desc_l, lu.tri_w, lu.tri_l, lu.burst_w, lu.burst_l};
+        for (int i = 0; i < 6; i++) {
+            unsigned long long x = v[i];
+            for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+            if ((threadIdx.x & 63u) == 0) atomicAdd(gl + i, x);
+        }
+    }
+#endif
     flush_counters(c, kp.stats);
     __syncthreads();
     if (tid < 4) cn->cls[tid] = lcnt[tid];
@@ -375,6 +431,14 @@ uint32_t wf_global_group_shift() {
 }
 
 }  // namespace
+
+#ifdef MCPT_PHASE_TIMING
+void read_lane_use_wf(unsigned long long out[6]) {   // wavefront extend lane-use counters, then reset
+    LaneUse z = {0, 0, 0, 0, 0, 0};
+    (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lane_use), sizeof z);
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_lane_use), &z, sizeof z);
+}
+#endif
 
 int wavefront_segments(uint32_t image_bytes, int cus) {
     return wf_in_lds(image_bytes) ? cus : cus * kGlobalBlocksPerCu;
