@@ -85,7 +85,8 @@ typedef struct {
     int32_t shard_index;
     int32_t packed;             /* 1: write owned tiles packed (tile-major) instead of row-major */
     int32_t pipeline;           /* MCPT_PIPELINE_*: megakernel (default) or wavefront; same image */
-    uint32_t wf_batch;          /* wavefront: max paths in flight per batch, 0 = 1<<25 */
+    uint32_t wf_batch;          /* wavefront: max paths in flight per batch (160 B of device
+                                   memory each), 0 = 1<<27, 1<<28 for scenes in global memory */
     int32_t mode;               /* MCPT_MODE_*: path semantics (default CVMCTracer)       */
     int32_t reserved_;          /* 0 */
 } mcpt_render_params;

@@ -394,10 +394,13 @@ Plan make_plan(const mcpt_scene& s, const mcpt_render_params* p) {
         throw mcpt::Error{MCPT_E_INVALID, "unknown pipeline"};
     pl.pipeline = p->pipeline;
     {
-        uint64_t cap = p->wf_batch ? p->wf_batch : (1u << 25);          // C2: 2^24 4.82, 2^25 5.07, 2^26 5.05
+        // default batch: big (160 B of queues per path; fewer launches, shorter
+        // relative tails).  C2 2^24 5.59, 2^25 6.43, 2^26 7.07, 2^27 7.31, 2^28 7.24;
+        // C4 (256 spp) 2^24 2.90, 2^26 3.45, 2^28 4.31 G rays/s
+        uint64_t cap = p->wf_batch ? p->wf_batch : (s.gpu.node_boxes ? (1u << 28) : (1u << 27));
         cap = std::max<uint64_t>(cap, chunk);                        // at least one pixel per batch
         cap = std::min<uint64_t>(cap, std::max<uint64_t>(npix, 1) * std::max<uint64_t>(p->spp, chunk));
-        cap = std::min<uint64_t>(cap, uint64_t(1) << 27);               // u32 slot arithmetic, 17 GB of queues
+        cap = std::min<uint64_t>(cap, uint64_t(1) << 28);               // u32 slot arithmetic; 160 B per path
         pl.wf_capacity = static_cast<uint32_t>(cap);
     }
     return pl;

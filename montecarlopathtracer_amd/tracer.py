@@ -170,7 +170,7 @@ class RenderParams:
     shard_index: int = 0
     packed: bool = False
     pipeline: str = "megakernel"      # or "wavefront" (C5): identical image, different kernels
-    wf_batch: int = 0                 # wavefront paths in flight per batch, 0 = 1<<25
+    wf_batch: int = 0                 # wavefront paths in flight per batch, 0 = 2^27 (2^28 global scenes)
     mode: str = "cvmctracer"          # or "quinengine": rtx.hlsl path semantics (see for_quinengine)
 
     @staticmethod
