@@ -68,7 +68,7 @@ def cpu_baseline(scene_name: str, width: int, height: int, seconds: float, threa
     spp = 8
     total_rays, total_t = 0, 0.0
     runs = 0
-    while total_t < seconds and runs < 64:
+    while total_t < seconds and runs < 1024:
         x0 = (width - crop) // 2 + (runs % 4) * 8
         y0 = (height - crop) // 2 + (runs // 4 % 4) * 8
         p = oracle.RenderParams(width=width, height=height, spp=spp, spp_chunk=32, spp_offset=runs * spp,
@@ -117,10 +117,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # MCPT_DIST_BACKEND=gloo: rehearsal of the N > 1 path with every rank on the
+    # GPUs this box has (local % device_count) and the gather staged through host
+    # memory; the driver's multi-GPU runs use the default, RCCL ("nccl").
+    backend = os.environ.get("MCPT_DIST_BACKEND", "nccl")
     if world > 1:
+        local = local % max(torch.cuda.device_count(), 1) if backend == "gloo" else local
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local if world > 1 else 0)
+    red_dev = dev if backend == "nccl" else torch.device("cpu")   # device of the small timing reductions
     torch.cuda.set_device(dev)
     M.Tracer().initialize([dev.index])
 
@@ -167,12 +176,12 @@ def main():
 
     rays = st["rays"]
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
         agg = torch.tensor([st[k] for k in ("rays", "paths", "inner_visits", "leaf_visits", "leaf_refs",
                                               "tri_tests", "shades")] + [st["kernel_ms"]],
-                           dtype=torch.float64, device=dev)
+                           dtype=torch.float64, device=red_dev)
         dist.all_reduce(agg, op=dist.ReduceOp.SUM)
         rays = int(agg[0].item())
 
@@ -186,7 +195,8 @@ def main():
         mray = rays / elapsed / 1e6
         workload = f"cornell_{args.width}x{args.height}_{args.spp}spp" + ("" if args.scene == "scene01" else
                                                                             f"_{args.scene}")
-        traffic, traffic_src = pmc_traffic(workload, args.pipeline)
+        # the committed PMC passes are single-GPU launches of the whole frame
+        traffic, traffic_src = pmc_traffic(workload, args.pipeline) if world == 1 else (None, None)
         line = {
             "metric": METRIC, "value": round(mray, 3), "unit": "Mray/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
@@ -195,7 +205,7 @@ def main():
             "config": {"workload": workload, "scene": args.scene,
                        "width": args.width, "height": args.height, "spp": args.spp, "max_depth": 7,
                        "spp_chunk": args.spp_chunk, "parallelism": f"pixel-tiles x{world}" +
-                       (" + rccl gather" if world > 1 else ""), "pipeline": args.pipeline,
+                       (f" + {'rccl' if backend == 'nccl' else backend} gather" if world > 1 else ""), "pipeline": args.pipeline,
                        "kernel_variant": st["variant"]},
             "rays_per_step": rays // args.steps,
             "rays_per_path": round(st["rays"] / max(st["paths"], 1), 4),

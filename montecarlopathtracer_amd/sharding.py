@@ -53,7 +53,15 @@ class TileGather:
         """fb_local: (n_local, 4) packed tiles of this rank. Returns the image on rank 0, None elsewhere."""
         import torch.distributed as dist
         self.send[: self.n_local].copy_(fb_local[: self.n_local])
-        dist.gather(self.send, self.recv if self.rank == 0 else None, dst=0)
+        if self.send.is_cuda and dist.get_backend() == "gloo":
+            # gloo has no device gather: stage through host memory (single-box rehearsal only)
+            recv = [r.cpu() for r in self.recv] if self.rank == 0 else None
+            dist.gather(self.send.cpu(), recv, dst=0)
+            if self.rank == 0:
+                for d, h in zip(self.recv, recv):
+                    d.copy_(h)
+        else:
+            dist.gather(self.send, self.recv if self.rank == 0 else None, dst=0)
         if self.rank != 0:
             return None
         for r in range(self.world):
