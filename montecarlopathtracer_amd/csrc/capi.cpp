@@ -86,6 +86,8 @@ struct Workspace {
     size_t fb_bytes = 0;
     void* wf = nullptr;          // wavefront queues / path state (one allocation)
     size_t wf_bytes = 0;
+    void* tail = nullptr;        // megakernel tail split: one float4 per tail sample
+    size_t tail_bytes = 0;
 };
 
 struct Timing {
@@ -115,7 +117,7 @@ struct mcpt_scene {
         (void)hipGetDevice(&prev);
         (void)hipSetDevice(device);
         (void)hipDeviceSynchronize();
-        for (void* p : {d_image, d_normals, ws.partial, ws.small, ws.spill, ws.fb, ws.wf})
+        for (void* p : {d_image, d_normals, ws.partial, ws.small, ws.spill, ws.fb, ws.wf, ws.tail})
             if (p) (void)hipFree(p);
         for (auto& t : pending) for (auto ev : t.e) (void)hipEventDestroy(ev);
         for (auto& t : free_timing) for (auto ev : t.e) (void)hipEventDestroy(ev);
@@ -354,6 +356,13 @@ Plan make_plan(const mcpt_scene& s, const mcpt_render_params* p) {
     k.spp = p->spp; k.spp_offset = p->spp_offset; k.chunk = chunk;
     k.nchunks = static_cast<uint32_t>(nchunks);
     k.total_units = static_cast<uint32_t>(npix * nchunks);
+    k.div_npix = mcpt::FastDiv::make(std::max<uint32_t>(k.npix_local, 1));
+    k.div_tt = mcpt::FastDiv::make(static_cast<uint32_t>(T * T));
+    k.div_tiles_x = mcpt::FastDiv::make(static_cast<uint32_t>(tiles_x));
+    k.div_tile = mcpt::FastDiv::make(static_cast<uint32_t>(T));
+    k.div_chunk = mcpt::FastDiv::make(chunk);
+    k.tail_units = k.total_units;         // no tail split unless prepare_workspace sets one
+    k.total_items = k.total_units;
     k.max_depth = p->max_depth;
     k.illum = p->illum;
     const float a = p->fov_deg * 3.14159265359f / 360;   // CUTracer.cu:189,202
@@ -406,7 +415,13 @@ Plan make_plan(const mcpt_scene& s, const mcpt_render_params* p) {
     return pl;
 }
 
-void prepare_workspace(mcpt_scene& s, mcpt::KernelParams& k) {
+// tail_split: the megakernel hands the last MCPT_TAIL_UNITS_PER_LANE (default
+// 6) units per lane of the work-unit order out one sample at a time
+// (KernelParams::tail_units).  Without it a lane's last whole unit (32 samples,
+// ~3.5 ms) set the kernel's end: at 1024 spp, rank 0 of 8 ran 64.4 ms against
+// 55.5 ideal (86%); split 2 / 4 / 6 / 8 / 12 per lane: 92 / 96 / 98 / 97 / 96%,
+// 1-GPU frame unchanged (442 -> 440 ms at 6).
+void prepare_workspace(mcpt_scene& s, mcpt::KernelParams& k, bool tail_split = false) {
     ensure_buf(s.ws.partial, s.ws.partial_bytes, size_t(k.nchunks) * k.npix_local * 16);
     if (!s.ws.small) {
         HIP_TRY(hipMalloc(&s.ws.small, 256));
@@ -418,6 +433,25 @@ void prepare_workspace(mcpt_scene& s, mcpt::KernelParams& k) {
     k.counter = static_cast<uint32_t*>(s.ws.small);
     k.stats = reinterpret_cast<unsigned long long*>(static_cast<char*>(s.ws.small) + 64);
     k.spill = static_cast<uint4*>(s.ws.spill);
+    k.tail_units = k.total_units;
+    k.total_items = k.total_units;
+    k.tail_buf = nullptr;
+    if (tail_split && k.chunk > 1) {
+        // MCPT_TAIL_UNITS: exact count (tests); MCPT_TAIL_UNITS_PER_LANE: per lane
+        const char* e = std::getenv("MCPT_TAIL_UNITS_PER_LANE");
+        const char* ea = std::getenv("MCPT_TAIL_UNITS");
+        const uint64_t per = e ? static_cast<uint64_t>(std::max(0, std::atoi(e))) : 6;
+        uint64_t tail = ea ? static_cast<uint64_t>(std::max(0LL, std::atoll(ea))) : per * lanes;
+        tail = std::min<uint64_t>(tail, k.total_units);
+        // item indices and tail slots stay below 2^31
+        while (tail && uint64_t(k.total_units - tail) + tail * k.chunk >= (uint64_t(1) << 31)) tail >>= 1;
+        if (tail) {
+            ensure_buf(s.ws.tail, s.ws.tail_bytes, size_t(tail) * k.chunk * 16);
+            k.tail_units = k.total_units - static_cast<uint32_t>(tail);
+            k.total_items = k.tail_units + static_cast<uint32_t>(tail * k.chunk);
+            k.tail_buf = static_cast<float4*>(s.ws.tail);
+        }
+    }
 }
 
 // wavefront workspace: 2 ray queues (o, d float4), hits, 4 class lists,
@@ -459,7 +493,8 @@ void render_async(mcpt_scene& s, const mcpt_render_params* p, float* d_fb, hipSt
     if (!d_fb) throw mcpt::Error{MCPT_E_INVALID, "framebuffer is NULL"};
     set_device(s);
     Plan pl = make_plan(s, p);
-    prepare_workspace(s, pl.kp);
+    // the tail split hands units out by sample, so per-unit counters need whole units
+    prepare_workspace(s, pl.kp, pl.pipeline == MCPT_PIPELINE_MEGAKERNEL && !d_unit_counters);
     pl.kp.unit_counters = d_unit_counters;
     Timing t;
     if (!s.free_timing.empty()) {
@@ -883,7 +918,7 @@ int mcpt_scene_reserve(mcpt_scene* s, const mcpt_render_params* p) {
         if (!s || !s->on_device) return fail(MCPT_E_INVALID, "scene is not on a device");
         set_device(*s);
         Plan pl = make_plan(*s, p);
-        prepare_workspace(*s, pl.kp);
+        prepare_workspace(*s, pl.kp, pl.pipeline == MCPT_PIPELINE_MEGAKERNEL);
         if (pl.pipeline == MCPT_PIPELINE_WAVEFRONT) (void)prepare_wavefront(*s, pl);
         return MCPT_OK;
     });

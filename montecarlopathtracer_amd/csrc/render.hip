@@ -37,6 +37,15 @@ namespace {
 // global variant (at 130 it lost a quarter of its occupancy: C4 -20%).  An
 // explicit min-waves bound (__launch_bounds__(BLOCK, 4)) made it slower (C4
 // 1.81 vs 1.97 G rays/s), so the budget is kept by the code instead.
+// sum of a unit's samples -> partial[chunk][v], or one tail sample's radiance
+__device__ __forceinline__ void store_part(const KernelParams& kp, uint32_t id, V3 part) {
+    const float4 val = make_float4(part.x, part.y, part.z, 0.0f);
+    if (id & 0x80000000u)
+        kp.tail_buf[id & 0x7FFFFFFFu] = val;
+    else
+        kp.partial[id] = val;
+}
+
 template <bool IN_LDS, int S, int BLOCK, bool DBG, bool QE>
 __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -120,7 +129,7 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
             if (!m) break;
             uint32_t unit;
             if constexpr (IN_LDS) {
-                unit = units.take(mode == kNeed, kp.counter);   // 64 units per atomic
+                unit = units.take(mode == kNeed, kp.counter);   // 64 items per atomic
             } else {
                 // scenes in global memory: units strictly in global order, one atomic
                 // per refill (C4 1.94 vs 1.69 G rays/s with 64-unit wave chunks)
@@ -130,21 +139,34 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
                 unit = __shfl(base, leader) + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
             }
             if (mode == kNeed) {
-                if (unit >= kp.total_units) {
+                if (unit >= kp.total_items) {
                     mode = kDead;
                 } else {
-                    unit_id = unit;
+                    // item -> unit u (+ one sample j of it in the tail split)
+                    uint32_t u = unit, j = 0, cnt = kp.chunk;
+                    const bool single = unit >= kp.tail_units;
+                    if (single) {
+                        const uint32_t k = unit - kp.tail_units;
+                        const uint32_t q = kp.div_chunk.div(k);
+                        u = kp.tail_units + q;
+                        j = k - q * kp.chunk;
+                        cnt = 1;
+                    }
+                    const uint32_t chunk = kp.div_npix.div(u);
+                    const uint32_t v = u - chunk * kp.npix_local;
+                    s = chunk * kp.chunk + j;
+                    s_end = min(s + cnt, kp.spp);
+                    // partial index, or the tail sample's slot with the top bit set
+                    unit_id = single ? (0x80000000u | (unit - kp.tail_units)) : u;
                     if constexpr (DBG) c0 = c;
-                    const uint32_t chunk = unit / kp.npix_local;
-                    const uint32_t v = unit - chunk * kp.npix_local;
-                    s = chunk * kp.chunk;
-                    s_end = min(s + kp.chunk, kp.spp);
                     part = v3(0, 0, 0);
-                    if (unit_pixel(kp, v, px, py)) {
+                    if (s >= s_end) {
+                        // sample past spp in a ragged last chunk: nothing to do, take another item
+                    } else if (unit_pixel(kp, v, px, py)) {
                         new_path();
                         start_ray();
                     } else {
-                        kp.partial[unit] = make_float4(0, 0, 0, 0);
+                        store_part(kp, unit_id, part);
                     }
                 }
             }
@@ -221,7 +243,7 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
                 part = vadd(part, L);
                 s++;
                 if (s == s_end) {
-                    kp.partial[unit_id] = make_float4(part.x, part.y, part.z, 0.0f);   // [chunk][v]
+                    store_part(kp, unit_id, part);
                     if constexpr (DBG) {
                         uint32_t* uc = kp.unit_counters + 4 * (size_t)unit_id;
                         uc[0] = c.rays - c0.rays;
@@ -269,8 +291,18 @@ __global__ void __launch_bounds__(256) reduce_kernel(const KernelParams kp, floa
     if (!unit_pixel(kp, v, x, y)) return;
     V3 sum = v3(0, 0, 0);
     for (uint32_t c = 0; c < kp.nchunks; c++) {
-        const float4 p = kp.partial[(size_t)c * kp.npix_local + v];
-        sum = vadd(sum, v3(p.x, p.y, p.z));
+        const uint32_t u = c * kp.npix_local + v;
+        V3 pc;
+        if (u >= kp.tail_units) {   // tail split: the unit's samples, in sample order
+            const float4* tb = kp.tail_buf + (size_t)(u - kp.tail_units) * kp.chunk;
+            const uint32_t n = min(kp.chunk, kp.spp - c * kp.chunk);
+            pc = v3(0, 0, 0);
+            for (uint32_t j = 0; j < n; j++) pc = vadd(pc, v3(tb[j].x, tb[j].y, tb[j].z));
+        } else {
+            const float4 p = kp.partial[u];
+            pc = v3(p.x, p.y, p.z);
+        }
+        sum = vadd(sum, pc);
     }
     const V3 mean = vdiv(sum, (float)kp.spp);
     const size_t idx = kp.packed ? (size_t)v : (size_t)y * (size_t)kp.width + (size_t)x;

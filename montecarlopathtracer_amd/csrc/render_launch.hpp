@@ -46,6 +46,28 @@ struct GpuScene {
     uint32_t root_w[2];                  // root node record (nodes[0])
 };
 
+// Unsigned division by a launch-invariant divisor d >= 1 as multiply-high and
+// shifts (Granlund & Montgomery 1994, fig. 4.1): exact for every 32-bit n.
+// The work-unit decode divides four times per unit; hardware has no integer
+// divide, and the generic sequence cost ~5% of C2 at 8-sample chunks.
+struct FastDiv {
+    uint32_t m, s1, s2, d;
+    static FastDiv make(uint32_t d) {
+        uint32_t l = 0;
+        while (l < 32 && (uint64_t(1) << l) < d) l++;          // ceil(log2 d)
+        FastDiv f;
+        f.m = static_cast<uint32_t>(((uint64_t(1) << 32) * ((uint64_t(1) << l) - d)) / d + 1);
+        f.s1 = l < 1 ? l : 1;
+        f.s2 = l > 0 ? l - 1 : 0;
+        f.d = d;
+        return f;
+    }
+    __host__ __device__ __forceinline__ uint32_t div(uint32_t n) const {
+        const uint32_t t = static_cast<uint32_t>((uint64_t(m) * n) >> 32);   // v_mul_hi_u32
+        return (t + ((n - t) >> s1)) >> s2;
+    }
+};
+
 struct KernelParams {
     GpuScene scene;
     int32_t width, height;
@@ -69,6 +91,15 @@ struct KernelParams {
     uint32_t lds_stack_off;              // LDS offset of the stack arrays
     uint32_t* unit_counters;             // optional [total_units][4]: rays, inner, leaf, tests
     int32_t ready_thresh;                // lanes ready before a shading round (1..64)
+    FastDiv div_npix, div_tt, div_tiles_x, div_tile;   // npix_local, tile^2, tiles_x, tile
+    // Tail split (megakernel): units [tail_units, total_units) -- the last
+    // ~6 per lane -- are handed out one sample at a time (work items
+    // tail_units + (u - tail_units) * chunk + j), each sample's radiance going
+    // to tail_buf[(u - tail_units) * chunk + j]; the reduction sums them in
+    // sample order, so the image is the one of whole units, bit for bit.
+    uint32_t tail_units, total_items;
+    FastDiv div_chunk;                   // chunk
+    float4* tail_buf;
 };
 
 // Wavefront pipeline workspace (wavefront.hip).  One batch = samples

@@ -297,11 +297,10 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
 
 // work unit v (packed owned-pixel index) -> image pixel; false outside the image
 __device__ __forceinline__ bool unit_pixel(const KernelParams& kp, uint32_t v, int& x, int& y) {
-    const uint32_t tt = (uint32_t)(kp.tile * kp.tile);
-    const uint32_t k = v / tt, w = v - k * tt;
+    const uint32_t k = kp.div_tt.div(v), w = v - k * kp.div_tt.d;
     const uint32_t t = (uint32_t)kp.shard_index + k * (uint32_t)kp.shard_count;
-    const uint32_t ty = t / (uint32_t)kp.tiles_x, tx = t - ty * (uint32_t)kp.tiles_x;
-    const uint32_t wy = w / (uint32_t)kp.tile, wx = w - wy * (uint32_t)kp.tile;
+    const uint32_t ty = kp.div_tiles_x.div(t), tx = t - ty * (uint32_t)kp.tiles_x;
+    const uint32_t wy = kp.div_tile.div(w), wx = w - wy * (uint32_t)kp.tile;
     x = (int)(tx * (uint32_t)kp.tile + wx);
     y = (int)(ty * (uint32_t)kp.tile + wy);
     return x < kp.width && y < kp.height;

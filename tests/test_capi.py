@@ -112,3 +112,15 @@ def test_struct_layouts_match_header(mcpt, tmp_path):
         assert int(out[cname]) == ctypes.sizeof(py), cname
         for f, _ in py._fields_:
             assert int(out[f"{cname}.{f}"]) == getattr(py, f).offset, (cname, f)
+
+
+def test_fastdiv_equals_integer_division():
+    """The work-unit decode's multiply-high division (render_launch.hpp FastDiv)
+    equals n / d: every divisor up to 70000 and 40000 random ones, dividends at
+    the edges, around multiples and random."""
+    import subprocess
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests", "cpp"))
+    import build_dropin
+    out = subprocess.run([build_dropin.build("fastdiv_probe")], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0 and out.stdout.strip() == "ok", out.stdout + out.stderr

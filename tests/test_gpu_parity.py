@@ -216,3 +216,23 @@ def test_qe_viewer_adapter_frames(mcpt, tmp_path):
         scene.render(mcpt.RenderParams.for_quinengine(width=W, height=H, seed=sd, prev_count=k), img)
     assert np.array_equal(got, img)
     assert np.array_equal(mcpt.read_png(png), mcpt.encode_8bit(img))
+
+
+@pytest.mark.parametrize("tail", ["0", "1000", "2100", None], ids=["whole-units", "mixed", "mixed-ragged", "default"])
+def test_tail_split_is_bit_identical(mcpt, oracle_mod, monkeypatch, tail):
+    """The megakernel's tail split (last units handed out one sample at a time,
+    summed in sample order by the reduction) renders the whole-unit image bit
+    for bit: no split, a split starting mid-chunk, and the default (every unit
+    of a small image).  spp 7 / chunk 3 leaves a ragged last chunk."""
+    if tail is None:
+        monkeypatch.delenv("MCPT_TAIL_UNITS", raising=False)
+    else:
+        monkeypatch.setenv("MCPT_TAIL_UNITS", tail)
+    path = mcpt.scene_path("scene01")
+    W, H, spp, chunk = 40, 30, 7, 3      # 1200 px x 3 chunks = 3600 units
+    ref, rc = _oracle_render(oracle_mod, path, W, H, spp, chunk, 7, 77, 1, 10.0, 1)
+    scene = mcpt.Scene(mcpt.ObjModel(path))
+    img, st = scene.render(mcpt.RenderParams.for_scene(1, width=W, height=H, spp=spp, spp_chunk=chunk, seed=77))
+    assert np.array_equal(img, ref), f"max abs diff {np.abs(img - ref).max()}"
+    for k in ("rays", "paths", "inner_visits", "leaf_visits", "leaf_refs", "tri_tests", "shades"):
+        assert st[k] == rc[k], (k, st[k], rc[k])
