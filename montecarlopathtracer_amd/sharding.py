@@ -40,14 +40,20 @@ class TileGather:
         self.recv = None
         self.image = None
         if rank == 0:
-            self.recv = [torch.zeros((self.maxn, 4), dtype=torch.float32, device=device) for _ in range(world)]
+            # one contiguous receive buffer (rank r's slots at r * maxn) and one
+            # precomputed slot -> pixel map: the unpermute is a single gather
+            # kernel with no host synchronisation
+            self.recv_all = torch.zeros((world * self.maxn, 4), dtype=torch.float32, device=device)
+            self.recv = list(self.recv_all.view(world, self.maxn, 4).unbind(0))
             self.image = torch.zeros((height * width, 4), dtype=torch.float32, device=device)
-            self.idx, self.valid = [], []
+            src, dst = [], []
             for r in range(world):
-                xy = torch.from_numpy(probe[r].shard_pixels().astype(np.int64)).to(device)
-                ok = xy[:, 0] >= 0
-                self.idx.append((xy[:, 1] * width + xy[:, 0])[ok])
-                self.valid.append(ok)
+                xy = probe[r].shard_pixels().astype(np.int64)
+                ok = np.nonzero(xy[:, 0] >= 0)[0]
+                src.append(r * self.maxn + ok)
+                dst.append(xy[ok, 1] * width + xy[ok, 0])
+            self.src = torch.from_numpy(np.concatenate(src)).to(device)
+            self.dst = torch.from_numpy(np.concatenate(dst)).to(device)
 
     def gather(self, fb_local) -> Optional["torch.Tensor"]:
         """fb_local: (n_local, 4) packed tiles of this rank. Returns the image on rank 0, None elsewhere."""
@@ -64,6 +70,5 @@ class TileGather:
             dist.gather(self.send, self.recv if self.rank == 0 else None, dst=0)
         if self.rank != 0:
             return None
-        for r in range(self.world):
-            self.image[self.idx[r]] = self.recv[r][: self.counts[r]][self.valid[r]]
+        self.image.index_copy_(0, self.dst, self.recv_all.index_select(0, self.src))
         return self.image
