@@ -230,7 +230,8 @@ def test_tail_split_is_bit_identical(mcpt, oracle_mod, monkeypatch, tail):
         monkeypatch.setenv("MCPT_TAIL_UNITS", tail)
     path = mcpt.scene_path("scene01")
     W, H, spp, chunk = 40, 30, 7, 3      # 1200 px x 3 chunks = 3600 units
-    ref, rc = _oracle_render(oracle_mod, path, W, H, spp, chunk, 7, 77, 1, 10.0, 1)
+    ref, rc = _oracle_render(oracle_mod, path, W, H, spp, chunk, 7, 77, 1, 10.0, 1,
+                             node_boxes=_node_boxes(mcpt, path))
     scene = mcpt.Scene(mcpt.ObjModel(path))
     img, st = scene.render(mcpt.RenderParams.for_scene(1, width=W, height=H, spp=spp, spp_chunk=chunk, seed=77))
     assert np.array_equal(img, ref), f"max abs diff {np.abs(img - ref).max()}"
