@@ -100,6 +100,10 @@ struct KernelParams {
     uint32_t tail_units, total_items;
     FastDiv div_chunk;                   // chunk
     float4* tail_buf;
+    // RNG seed table (megakernel): seeds[u * chunk + j] = path_seed of sample j
+    // of unit u, written by seed_kernel before the path kernel (nullptr: the
+    // path kernel computes TEA-16 itself)
+    const uint32_t* seeds;
 };
 
 // Wavefront pipeline workspace (wavefront.hip).  One batch = samples

@@ -306,10 +306,8 @@ __device__ __forceinline__ bool unit_pixel(const KernelParams& kp, uint32_t v, i
     return x < kp.width && y < kp.height;
 }
 
-// primary ray of sample s of pixel (px, py) (CUTracer.cu:186-211)
-__device__ __forceinline__ void primary_ray(const KernelParams& kp, uint32_t pix, int px, int py, uint32_t s,
-                                            uint32_t& sd, V3& dir) {
-    sd = rng_init(pix, kp.key, kp.spp_offset + s);
+// primary ray of pixel (px, py) from its sample's RNG seed sd (CUTracer.cu:186-211)
+__device__ __forceinline__ void primary_ray_sd(const KernelParams& kp, int px, int py, uint32_t& sd, V3& dir) {
     const float biasx = (float)(uint32_t)px + (rng_next(sd) * 2.0f - 1.0f);
     const float biasy = (float)(uint32_t)py + (rng_next(sd) * 2.0f - 1.0f);
     const double th = (double)kp.tan_half_fov;
@@ -323,6 +321,12 @@ __device__ __forceinline__ void primary_ray(const KernelParams& kp, uint32_t pix
     wr.z = kp.right[2] * idx + kp.up[2] * idy - kp.fwd[2] * idz;
     normalize_cu(wr);
     dir = wr;
+}
+// primary ray of sample s of pixel (px, py)
+__device__ __forceinline__ void primary_ray(const KernelParams& kp, uint32_t pix, int px, int py, uint32_t s,
+                                            uint32_t& sd, V3& dir) {
+    sd = rng_init(pix, kp.key, kp.spp_offset + s);
+    primary_ray_sd(kp, px, py, sd, dir);
 }
 
 
@@ -443,9 +447,8 @@ constexpr float kQeGamma = 2.2f;
 constexpr float kQeInvGamma = 0.454545454545f;   // 1 / 2.2 as float
 // primary ray: TEA-16(pixel, frame seed) + two warm-up draws, +-0.5 px jitter,
 // origin on the near plane z = -1 of the view, view -> world by the basis
-__device__ __forceinline__ void primary_ray_qe(const KernelParams& kp, uint32_t pix, int px, int py, uint32_t s,
-                                               uint32_t& sd, V3& o, V3& dir) {
-    sd = tea16(pix, kp.key + kp.spp_offset + s);
+__device__ __forceinline__ void primary_ray_qe_sd(const KernelParams& kp, int px, int py, uint32_t& sd, V3& o,
+                                                  V3& dir) {
     (void)rng_next(sd);
     (void)rng_next(sd);
     const float bx = (float)(uint32_t)px + (rng_next(sd) - 0.5f);
@@ -460,6 +463,15 @@ __device__ __forceinline__ void primary_ray_qe(const KernelParams& kp, uint32_t 
     o = v3(w.x + kp.eye[0], w.y + kp.eye[1], w.z + kp.eye[2]);
     normalize_cu(w);
     dir = w;
+}
+__device__ __forceinline__ void primary_ray_qe(const KernelParams& kp, uint32_t pix, int px, int py, uint32_t s,
+                                               uint32_t& sd, V3& o, V3& dir) {
+    sd = tea16(pix, kp.key + kp.spp_offset + s);
+    primary_ray_qe_sd(kp, px, py, sd, o, dir);
+}
+// RNG seed of sample s of pixel pix: rng_init (CV) or the TEA-16 state (QE)
+__device__ __forceinline__ uint32_t path_seed(const KernelParams& kp, uint32_t pix, uint32_t s) {
+    return kp.mode == kModeQE ? tea16(pix, kp.key + kp.spp_offset + s) : rng_init(pix, kp.key, kp.spp_offset + s);
 }
 // Russian roulette from bounce `depth` on (rtx.hlsl:314-325); false = path dies
 __device__ __forceinline__ bool qe_roulette(uint32_t& sd, V3& color) {
