@@ -304,15 +304,29 @@ __global__ void __launch_bounds__(256) seed_kernel(const KernelParams kp, uint4*
     for (uint32_t q = blockIdx.x * 256u + threadIdx.x; q < nq; q += gridDim.x * 256u) {
         uint32_t pix[4], smp[4];
         bool ok[4];
-#pragma unroll
-        for (int e = 0; e < 4; e++) {
-            const uint32_t i = 4u * q + (uint32_t)e;
+        if ((kp.chunk & 3u) == 0u) {          // the quad lies in one unit: decode it once
+            const uint32_t i = 4u * q;
             const uint32_t u = kp.div_chunk.div(i), j = i - u * kp.chunk;
             const uint32_t ch = kp.div_npix.div(u), v = u - ch * kp.npix_local;
-            smp[e] = ch * kp.chunk + j;
             int x = 0, y = 0;
-            ok[e] = i < n && smp[e] < kp.spp && unit_pixel(kp, v, x, y);
-            pix[e] = (uint32_t)y * (uint32_t)kp.width + (uint32_t)x;
+            const bool in = i < n && unit_pixel(kp, v, x, y);
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                smp[e] = ch * kp.chunk + j + (uint32_t)e;
+                ok[e] = in && smp[e] < kp.spp;
+                pix[e] = (uint32_t)y * (uint32_t)kp.width + (uint32_t)x;
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const uint32_t i = 4u * q + (uint32_t)e;
+                const uint32_t u = kp.div_chunk.div(i), j = i - u * kp.chunk;
+                const uint32_t ch = kp.div_npix.div(u), v = u - ch * kp.npix_local;
+                smp[e] = ch * kp.chunk + j;
+                int x = 0, y = 0;
+                ok[e] = i < n && smp[e] < kp.spp && unit_pixel(kp, v, x, y);
+                pix[e] = (uint32_t)y * (uint32_t)kp.width + (uint32_t)x;
+            }
         }
         uint32_t sd[4];
 #pragma unroll

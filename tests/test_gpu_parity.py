@@ -237,3 +237,27 @@ def test_tail_split_is_bit_identical(mcpt, oracle_mod, monkeypatch, tail):
     assert np.array_equal(img, ref), f"max abs diff {np.abs(img - ref).max()}"
     for k in ("rays", "paths", "inner_visits", "leaf_visits", "leaf_refs", "tri_tests", "shades"):
         assert st[k] == rc[k], (k, st[k], rc[k])
+
+
+@pytest.mark.parametrize("mode", ["cv", "qe"])
+def test_seed_table_matches_in_kernel_seeding(mcpt, oracle_mod, monkeypatch, mode):
+    """The megakernel's RNG seed table (seed_kernel, next seed prefetched) and the
+    in-kernel TEA-16 fallback (MCPT_SEED_TABLE=0) render the oracle's image bit for
+    bit, with ragged chunks and the tail split active."""
+    path = mcpt.scene_path("scene01")
+    W, H, spp, chunk = 36, 28, 9, 4
+    if mode == "qe":
+        ref, rc = oracle_mod.Scene(path).render(oracle_mod.RenderParams(
+            width=W, height=H, spp=spp, spp_chunk=chunk, max_depth=5, seed=31, illum=1.0, fov=45.0, fresnel_kd=0,
+            threads=8, mode=oracle_mod.MODE_QE, node_boxes=_node_boxes(mcpt, path)))
+        p = _qe_params(mcpt, W, H, spp, chunk, 5, 31)
+    else:
+        ref, rc = _oracle_render(oracle_mod, path, W, H, spp, chunk, 7, 31, 1, 10.0, 1, node_boxes=_node_boxes(mcpt, path))
+        p = mcpt.RenderParams.for_scene(1, width=W, height=H, spp=spp, spp_chunk=chunk, seed=31)
+    scene = mcpt.Scene(mcpt.ObjModel(path))
+    for table in ("1", "0"):
+        monkeypatch.setenv("MCPT_SEED_TABLE", table)
+        img, st = scene.render(p)
+        assert np.array_equal(img, ref), (table, float(np.abs(img - ref).max()))
+        for k in ("rays", "paths", "inner_visits", "leaf_visits", "leaf_refs", "tri_tests", "shades"):
+            assert st[k] == rc[k], (table, k, st[k], rc[k])
