@@ -2,9 +2,10 @@
 //
 // Arithmetic contract (DESIGN.md "Determinism spec"): every float expression
 // keeps the reference's operand order and is compiled with -ffp-contract=off;
-// division and sqrt are IEEE correctly rounded (HIP default); sin/cos/pow are
-// fixed double-precision sequences built from add/mul/div/floor and bit casts
-// only, so the HIP kernel reproduces the CPU specification bit for bit.
+// division and sqrt are IEEE correctly rounded (HIP default); sin/cos are a
+// fixed float sequence, pow a fixed double one and the Fresnel x^5 three double
+// multiplies -- add/mul/div/floor and bit casts only -- so the HIP kernel
+// reproduces the CPU specification bit for bit.
 //
 // Reference lines restated here:
 //   det()                 CVMCTracer/Framework/Math.hpp:169-175
@@ -47,36 +48,27 @@ __device__ __forceinline__ float sqrt_rn(float x) { return __builtin_sqrtf(x); }
 __device__ __forceinline__ uint64_t d2u(double x) { return __builtin_bit_cast(uint64_t, x); }
 __device__ __forceinline__ double u2d(uint64_t u) { return __builtin_bit_cast(double, u); }
 
-__device__ __forceinline__ double sin_poly(double r) {
-    const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
-                 S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
-                 S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
-    double z = r * r;
-    double v = z * r;
-    double p = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
-    return r + v * (S1 + z * p);
+// sin and cos in float arithmetic only: Cody-Waite pi/2 reduction in three
+// parts (exact for the samplers' [0, 2pi)), Cephes sinf/cosf minimax
+// polynomials on [-pi/4, pi/4]; <= 2 ulp (sin) / 1 ulp (cos) against libm on
+// [0, 2pi).  The earlier double-precision (fdlibm) sequences cost 2.6% of the
+// C2 frame.  Oracle: mc_sincos_f.
+__device__ __forceinline__ void sincos_f(float x, float& s, float& c) {
+    const float k = __builtin_floorf(x * 0.636619772367581343f + 0.5f);
+    const float r = ((x - k * 1.5703125f) - k * 4.837512969970703125e-4f) - k * 7.54978995489188216e-8f;
+    const float z = r * r;
+    const float sr = ((-1.9515295891e-4f * z + 8.3321608736e-3f) * z - 1.6666654611e-1f) * z * r + r;
+    const float cr = ((2.443315711809948e-5f * z - 1.388731625493765e-3f) * z + 4.166664568298827e-2f) * z * z -
+                     0.5f * z + 1.0f;
+    const int q = (int)(k - 4.0f * __builtin_floorf(k * 0.25f));   // k mod 4, exact
+    s = q == 0 ? sr : (q == 1 ? cr : (q == 2 ? -sr : -cr));
+    c = q == 0 ? cr : (q == 1 ? -sr : (q == 2 ? -cr : sr));
 }
-__device__ __forceinline__ double cos_poly(double r) {
-    const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
-                 C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
-                 C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
-    double z = r * r;
-    double p = z * (C1 + z * (C2 + z * (C3 + z * (C4 + z * (C5 + z * C6)))));
-    return 1.0 - (0.5 * z - z * p);
-}
-__device__ __forceinline__ void sincos_f(float xf, float& s, float& c) {
-    const double INV_PIO2 = 6.36619772367581382433e-01;
-    const double PIO2_1 = 1.57079632673412561417e+00;
-    const double PIO2_1T = 6.07710050650619224932e-11;
-    double x = (double)xf;
-    double k = __builtin_floor(x * INV_PIO2 + 0.5);
-    double r = (x - k * PIO2_1) - k * PIO2_1T;
-    double sr = sin_poly(r), cr = cos_poly(r);
-    int q = ((int)k) & 3;
-    double sd = (q == 0) ? sr : (q == 1) ? cr : (q == 2) ? -sr : -cr;
-    double cd = (q == 0) ? cr : (q == 1) ? -sr : (q == 2) ? -cr : sr;
-    s = (float)sd;
-    c = (float)cd;
+// x^5 of the Fresnel term (Utils.hpp:101) in double, rounded once to float
+// (x^2 exact in double): within 1 ulp, three multiplies instead of log/exp
+__device__ __forceinline__ float pow5_f(float x) {
+    const double d = (double)x, d2 = d * d;
+    return (float)(d2 * d2 * d);
 }
 __device__ __forceinline__ double log2_d(double x) {
     uint64_t b = d2u(x);
@@ -199,7 +191,7 @@ __device__ __forceinline__ V3 sample_fresnel(uint32_t& sd, V3 n, V3 in, float Tr
     float x = rng_next(sd);
     V3 out;
     float ndoti = dot3(in, n);
-    Tr = Tr * (1 - pow_f(1 - fabsf(ndoti), 5.0f));
+    Tr = Tr * (1 - pow5_f(1 - fabsf(ndoti)));
     if (x < Tr) {
         if (ndoti <= 0) {
             float alpha = -ndoti / Ni - sqrt_rn(1 - (1 - ndoti * ndoti) / Ni / Ni);

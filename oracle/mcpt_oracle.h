@@ -29,7 +29,7 @@
  *     TEA-16 seeding + Park-Miller/Schrage (QE/Shader/rtx.hlsl:61-82), keyed
  *     statelessly per (pixel, sample).
  *   - sinf/cosf/powf: device libm differs from glibc by ulps; both sides use
- *     the fixed double-precision sequences in this file (mc_sin_d etc.).
+ *     the fixed sequences in this file (float sin/cos, double pow and x^5).
  *   - KD "ordered" mode (traversal == 2): the exact traversal order the HIP
  *     kernel uses, so node/triangle counts and tie-breaks are comparable
  *     bit for bit.  Its closest hit equals brute force except on exact t ties.
@@ -112,6 +112,7 @@ uint32_t orc_seed_key(uint64_t seed);
 float orc_sinf(float x);
 float orc_cosf(float x);
 float orc_powf(float x, float y);
+float orc_pow5f(float x);                                        /* Fresnel (1-|n.d|)^5 */
 /* samplers with injected uniforms: u = uniforms consumed in order */
 void orc_sample_hemi(const float* n, const float* u, float* out);
 void orc_sample_phong(const float* n, const float* in, uint32_t Ns, const float* u, float* out);

@@ -87,6 +87,8 @@ def lib():
             getattr(L, n).argtypes = [C.c_float]
         L.orc_powf.restype = C.c_float
         L.orc_powf.argtypes = [C.c_float, C.c_float]
+        L.orc_pow5f.restype = C.c_float
+        L.orc_pow5f.argtypes = [C.c_float]
         L.orc_sample_hemi.argtypes = [f32p, f32p, f32p]
         L.orc_sample_phong.argtypes = [f32p, f32p, C.c_uint32, f32p, f32p]
         L.orc_sample_fresnel.argtypes = [f32p, f32p, C.c_float, C.c_float, f32p, f32p]

@@ -26,44 +26,37 @@
 #define KD_EPS_LO 0.999755859375f   /* 1 - 2^-12 */
 
 /* ======================= deterministic transcendentals ===================== */
-/* The same double-precision operation sequence is compiled into the HIP
- * kernel (montecarlopathtracer_amd/csrc/mcpt_device_math.hpp); only IEEE
- * add/mul/div, floor and bit casts are used, so CPU and GPU agree bitwise.  */
+/* The same operation sequences are compiled into the HIP kernel
+ * (montecarlopathtracer_amd/csrc/mcpt_device.hpp); only IEEE add/mul/div,
+ * floor and bit casts are used, so CPU and GPU agree bitwise.               */
 static inline uint64_t d2u(double x) { uint64_t u; memcpy(&u, &x, 8); return u; }
 static inline double u2d(uint64_t u) { double x; memcpy(&x, &u, 8); return x; }
 
-static double mc_sin_poly(double r) {
-    const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
-                 S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
-                 S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
-    double z = r * r;
-    double v = z * r;
-    double p = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
-    return r + v * (S1 + z * p);
-}
-static double mc_cos_poly(double r) {
-    const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
-                 C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
-                 C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
-    double z = r * r;
-    double p = z * (C1 + z * (C2 + z * (C3 + z * (C4 + z * (C5 + z * C6)))));
-    return 1.0 - (0.5 * z - z * p);
-}
-static void mc_sincos_d(double x, double* s, double* c) {
-    const double INV_PIO2 = 6.36619772367581382433e-01;
-    const double PIO2_1 = 1.57079632673412561417e+00;
-    const double PIO2_1T = 6.07710050650619224932e-11;
-    double k = floor(x * INV_PIO2 + 0.5);
-    double r = (x - k * PIO2_1) - k * PIO2_1T;
-    double sr = mc_sin_poly(r), cr = mc_cos_poly(r);
-    int q = ((int)k) & 3;
+/* sin and cos in float arithmetic only: Cody-Waite pi/2 reduction in three
+ * parts (exact for the samplers' [0, 2pi)), Cephes sinf/cosf minimax
+ * polynomials on [-pi/4, pi/4].  <= 2 ulp (sin) / 1 ulp (cos) against libm
+ * on [0, 2pi); mcpt_device.hpp sincos_f performs the same float operations. */
+static void mc_sincos_f(float x, float* s, float* c) {
+    const float k = floorf(x * 0.636619772367581343f + 0.5f);
+    const float r = ((x - k * 1.5703125f) - k * 4.837512969970703125e-4f) - k * 7.54978995489188216e-8f;
+    const float z = r * r;
+    const float sr = ((-1.9515295891e-4f * z + 8.3321608736e-3f) * z - 1.6666654611e-1f) * z * r + r;
+    const float cr = ((2.443315711809948e-5f * z - 1.388731625493765e-3f) * z + 4.166664568298827e-2f) * z * z -
+                     0.5f * z + 1.0f;
+    const int q = (int)(k - 4.0f * floorf(k * 0.25f));   /* k mod 4, exact */
     if (q == 0) { *s = sr; *c = cr; }
     else if (q == 1) { *s = cr; *c = -sr; }
     else if (q == 2) { *s = -sr; *c = -cr; }
     else { *s = -cr; *c = sr; }
 }
-float orc_sinf(float x) { double s, c; mc_sincos_d((double)x, &s, &c); return (float)s; }
-float orc_cosf(float x) { double s, c; mc_sincos_d((double)x, &s, &c); return (float)c; }
+float orc_sinf(float x) { float s, c; mc_sincos_f(x, &s, &c); return s; }
+float orc_cosf(float x) { float s, c; mc_sincos_f(x, &s, &c); return c; }
+/* x^5 of the Fresnel term (Utils.hpp:101) in double, rounded once to float:
+ * x^2 is exact in double, so the result is within 1 ulp (mcpt_device.hpp pow5_f) */
+float orc_pow5f(float x) {
+    const double d = (double)x, d2 = d * d;
+    return (float)(d2 * d2 * d);
+}
 
 static double mc_log2_d(double x) {   /* x: positive finite (from a float) */
     uint64_t b = d2u(x);
@@ -205,7 +198,7 @@ static orc_v3 sample_fresnel(usrc* u, orc_v3 n, orc_v3 in, float Tr, float Ni) {
     float x = next_u(u);
     orc_v3 out;
     float ndoti = dot3(in, n);
-    Tr = Tr * (1 - orc_powf(1 - fabsf(ndoti), 5));
+    Tr = Tr * (1 - orc_pow5f(1 - fabsf(ndoti)));
     if (x < Tr) {
         if (ndoti <= 0) {
             float alpha = -ndoti / Ni - sqrtf(1 - (1 - ndoti * ndoti) / Ni / Ni);

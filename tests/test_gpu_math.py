@@ -1,6 +1,6 @@
 """Device math of the product (csrc/mcpt_device.hpp) against the CPU
 specification, bit for bit: IEEE float/double division and sqrt, the fixed
-double-precision sin/cos/pow sequences, the TEA-16/Park-Miller RNG."""
+sin/cos (float) and pow / x^5 (double) sequences, the TEA-16/Park-Miller RNG."""
 import ctypes as C
 import os
 import sys
@@ -79,6 +79,9 @@ def test_sincos_pow_match_spec(probe, oracle_mod):
     o, _, _ = probe(4, x, y)
     ref = np.array([L.orc_powf(float(a), float(b)) for a, b in zip(x, y)], np.float32)
     assert np.array_equal(o, ref)
+    o5, _, _ = probe(11, x, x)
+    ref5 = np.array([L.orc_pow5f(float(a)) for a in x], np.float32)
+    assert np.array_equal(o5, ref5)
 
 
 def test_rng_matches_spec(probe, oracle_mod):
