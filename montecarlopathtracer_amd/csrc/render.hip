@@ -406,12 +406,6 @@ hipError_t launch_render(const KernelParams& kp_in, int cus, hipStream_t st, hip
     }
     if (ev0) hipEventRecord(ev0, st);
     int variant = 0;
-#ifdef MCPT_EXP_S2   // timing experiment: shallower LDS stack
-    if (true) {
-        variant = 2;
-        e = launch_path<true, 2, kLdsBlock>(kp, cus, lds_bytes_in_lds(img, 2), st);
-    } else
-#endif
     if (kp.scene.node_boxes) {                     // image built for global memory
         variant = 3;
         e = launch_path<false, 8, kGlobalBlock>(kp, cus * kGlobalBlocksPerCu, (size_t)8 * kGlobalBlock * 16, st);

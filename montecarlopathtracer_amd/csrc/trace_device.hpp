@@ -369,11 +369,7 @@ __device__ __forceinline__ void scatter_n(const GpuGeom& g, float4 n1, float4 n2
 __device__ __forceinline__ void scatter(const GpuGeom& g, const float4* __restrict__ normals, int32_t htri,
                                         float hbeta, float hgamma, float best, int32_t fresnel_kd, uint32_t& sd,
                                         V3& color, V3& o, V3& d) {
-#ifdef MCPT_EXP_NONORMAL   // timing experiment only: no global normal fetch (wrong image)
-    const float4 n1 = make_float4(0.0f, 1.0f, 0.0f, 0.0f), n2 = n1, n3 = make_float4(hbeta, 1.0f, hgamma, 0.0f);
-#else
     const float4 n1 = normals[3 * htri], n2 = normals[3 * htri + 1], n3 = normals[3 * htri + 2];
-#endif
     scatter_n(g, n1, n2, n3, hbeta, hgamma, best, fresnel_kd, sd, color, o, d);
 }
 // material class of a geometry for the wavefront's per-material queues
