@@ -101,8 +101,7 @@ __device__ __forceinline__ bool begin_ray(RayState& r, const GpuScene& sc, float
 // the three IEEE divisions run only when the signs of the determinants allow
 // beta, gamma, t > 0 and the magnitudes do not already rule out beta+gamma < 1
 // or t < best (2^-20 margins cover every rounding of the exact path).
-__device__ __forceinline__ void test_tri(RayState& r, const float4* __restrict__ tris, uint32_t k) {
-    const float4 A0 = tris[3 * k], A1 = tris[3 * k + 1], A2 = tris[3 * k + 2];
+__device__ __forceinline__ void test_tri_v(RayState& r, const float4 A0, const float4 A1, const float4 A2, uint32_t k) {
     const float aox = A0.x - r.o.x, aoy = A0.y - r.o.y, aoz = A0.z - r.o.z;
     const float detA = det3(A1.x, A2.x, r.d.x, A1.y, A2.y, r.d.y, A1.z, A2.z, r.d.z);
     const float qb = det3(aox, A2.x, r.d.x, aoy, A2.y, r.d.y, aoz, A2.z, r.d.z);
@@ -132,6 +131,9 @@ __device__ __forceinline__ void test_tri(RayState& r, const float4* __restrict__
         }
     }
 }
+__device__ __forceinline__ void test_tri(RayState& r, const float4* __restrict__ tris, uint32_t k) {
+    test_tri_v(r, tris[3 * k], tris[3 * k + 1], tris[3 * k + 2], k);
+}
 
 // One resumable traversal iteration: descend to a leaf, test it, pop.
 // Returns true when the ray's closest hit is final.  The children of the
@@ -157,6 +159,9 @@ __device__ __forceinline__ void test_tri(RayState& r, const float4* __restrict__
 #endif
 #ifndef MCPT_TRI_CAP
 #define MCPT_TRI_CAP 2
+#endif
+#ifndef MCPT_TRI_PAIR
+#define MCPT_TRI_PAIR 1
 #endif
 constexpr int kDescentCap = MCPT_DESCENT_CAP;
 constexpr uint32_t kTriCap = MCPT_TRI_CAP;
@@ -310,12 +315,37 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
         r.lpos = w0 & 0x3FFFFFFFu;
         r.lend = r.lpos + w1;
     }
+#if MCPT_TRI_PAIR
+    static_assert(kTriCap == 2, "paired triangle tests assume a cap of 2");
+    if (r.lpos < r.lend) {
+        // both triangles' records are read before either test runs, so the two
+        // LDS round trips (leaf ref -> triangle) overlap instead of chaining; a
+        // leaf's last single triangle re-reads its own record as the second one
+        // (in bounds: the ref after a leaf section's end is image padding/geoms)
+        const bool two = r.lend - r.lpos >= 2u;
+        const uint32_t k0 = leafs[r.lpos], k1n = leafs[r.lpos + 1u];
+        const uint32_t k1 = two ? k1n : k0;
+        const float4 a0 = tris[3 * k0], a1 = tris[3 * k0 + 1], a2 = tris[3 * k0 + 2];
+        const float4 b0 = tris[3 * k1], b1 = tris[3 * k1 + 1], b2 = tris[3 * k1 + 2];
+        MCPT_LANE_USE(tri_w, tri_l, lu);
+        c.refs++;
+        c.tests++;
+        test_tri_v(r, a0, a1, a2, k0);
+        if (two) {
+            c.refs++;
+            c.tests++;
+            test_tri_v(r, b0, b1, b2, k1);
+        }
+        r.lpos += two ? 2u : 1u;
+    }
+#else
     for (uint32_t i = 0; i < kTriCap && r.lpos < r.lend; i++, r.lpos++) {
         c.refs++;
         MCPT_LANE_USE(tri_w, tri_l, lu);
         c.tests++;
         test_tri(r, tris, leafs[r.lpos]);
     }
+#endif
     if (r.lpos < r.lend) return false;        // more triangles in this leaf
     return !pop_entry<S, !BOXES>(r, st, stride, spill, spill_stride);
 }
