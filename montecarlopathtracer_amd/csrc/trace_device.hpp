@@ -205,9 +205,10 @@ __device__ __forceinline__ bool box_hit(const RayState& r, uint32_t b0, uint32_t
 // waits for a refill it may never use (C2 +0.9%, spills/ray 0.32 -> see bench).
 // Eager (global-memory scenes, 8-entry LDS part, spills rare): the freed slot
 // is refilled at once.
+// `top`, if given, is the LDS slot of the top entry read ahead by the caller.
 template <int S, bool LAZY>
 __device__ __forceinline__ bool pop_entry(RayState& r, uint4* st, int stride, uint4* __restrict__ spill,
-                                          uint32_t spill_stride) {
+                                          uint32_t spill_stride, const uint4* top = nullptr) {
     if (r.sp == 0) return false;
     r.sp--;
     uint4 e;
@@ -216,11 +217,11 @@ __device__ __forceinline__ bool pop_entry(RayState& r, uint4* st, int stride, ui
             e = spill[(uint32_t)r.sp * spill_stride];
             r.lo = r.sp;
         } else {
-            e = st[(r.sp & (S - 1)) * stride];
+            e = top ? *top : st[(r.sp & (S - 1)) * stride];
         }
     } else {                                  // refill the freed slot with the next older entry
         uint4* slot = st + (r.sp & (S - 1)) * stride;
-        e = *slot;
+        e = top ? *top : *slot;
         if (r.sp >= S) *slot = spill[(uint32_t)(r.sp - S) * spill_stride];
     }
     r.nw0 = e.x;
@@ -317,6 +318,10 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
     }
 #if MCPT_TRI_PAIR
     static_assert(kTriCap == 2, "paired triangle tests assume a cap of 2");
+    // the stack's top slot, read ahead: the pop after this leaf's last tests
+    // then needs no LDS round trip of its own (unused if the leaf goes on or
+    // the stack is empty -- the slot index is in range either way)
+    const uint4 top = st[((r.sp - 1) & (S - 1)) * stride];
     if (r.lpos < r.lend) {
         // both triangles' records are read before either test runs, so the two
         // LDS round trips (leaf ref -> triangle) overlap instead of chaining; a
@@ -347,7 +352,11 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
     }
 #endif
     if (r.lpos < r.lend) return false;        // more triangles in this leaf
+#if MCPT_TRI_PAIR
+    return !pop_entry<S, !BOXES>(r, st, stride, spill, spill_stride, &top);
+#else
     return !pop_entry<S, !BOXES>(r, st, stride, spill, spill_stride);
+#endif
 }
 
 // work unit v (packed owned-pixel index) -> image pixel; false outside the image
