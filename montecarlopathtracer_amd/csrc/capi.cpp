@@ -222,7 +222,10 @@ void build_image(mcpt_scene& s) {
         if (boxes) ol = al16(on + size_t((o.n_slots - 1) / 2) * 48);   // pair m: device nodes 2m+1, 2m+2
         else ol = al16(on + size_t(o.n_slots + 1) * 8);                 // node slot j = device node j-1
         og = al16(ol + size_t(nl) * 4);
-        return al16(og + size_t(ng) * 64);
+        // (geometries never empty for a scene with triangles; the paired
+        // triangle tests read the ref after a leaf's last one, so the leaf
+        // section must never end the image)
+        return al16(og + size_t(std::max<uint32_t>(ng, 1u)) * 64);
     };
     size_t off_nodes, off_leafs, off_geoms;
     size_t total = image_size(ord, off_nodes, off_leafs, off_geoms);
