@@ -447,8 +447,20 @@ void prepare_workspace(mcpt_scene& s, mcpt::KernelParams& k, bool tail_split = f
     const uint64_t seed_entries = uint64_t(k.total_units) * k.chunk;
     const char* es = std::getenv("MCPT_SEED_TABLE");
     if (tail_split && seed_entries > 0 && seed_entries < (uint64_t(1) << 31) && !(es && std::atoi(es) == 0)) {
-        ensure_buf(s.ws.seeds, s.ws.seeds_bytes, size_t((seed_entries + 3) / 4) * 16);   // seed_kernel: 4 per store
-        k.seeds = static_cast<const uint32_t*>(s.ws.seeds);
+        // the table is an optimisation: without the memory for it, seed in place
+        const size_t need = size_t((seed_entries + 3) / 4) * 16;              // seed_kernel: 4 per store
+        if (s.ws.seeds_bytes < need || !s.ws.seeds) {
+            if (s.ws.seeds) HIP_TRY(hipFree(s.ws.seeds));
+            s.ws.seeds = nullptr;
+            s.ws.seeds_bytes = 0;
+            if (hipMalloc(&s.ws.seeds, need) == hipSuccess) {
+                s.ws.seeds_bytes = need;
+            } else {
+                s.ws.seeds = nullptr;
+                (void)hipGetLastError();                                    // clear the sticky error
+            }
+        }
+        if (s.ws.seeds) k.seeds = static_cast<const uint32_t*>(s.ws.seeds);
     }
     if (tail_split && k.chunk > 1) {
         // MCPT_TAIL_UNITS: exact count (tests); MCPT_TAIL_UNITS_PER_LANE: per lane
