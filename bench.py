@@ -16,6 +16,7 @@ Launch:  python bench.py [--gpus 1 --steps 3 --warmup 1]
 from __future__ import annotations
 
 import argparse
+import dataclasses
 import json
 import os
 import sys
@@ -108,6 +109,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = this process's CPU share (<= 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--counting", action="store_true", help="time the counting megakernel instead of the lean one")
     args = ap.parse_args()
 
     import torch
@@ -135,9 +137,14 @@ def main():
 
     scene = M.Scene(M.ObjModel(M.scene_path(args.scene)))
     scene_id = 2 if args.scene in ("scene02", "scene03") else 1
+    # timed renders run the megakernel lean (no per-step traversal counters, same
+    # image and ray count); the node/leaf/triangle counts of the bytes model come
+    # from one untimed counting render of the same frame (they are deterministic)
+    lean = args.pipeline == "megakernel" and not args.counting
     p = M.RenderParams.for_scene(scene_id, width=args.width, height=args.height, spp=args.spp,
                                  spp_chunk=args.spp_chunk, tile=8, shard_count=world, shard_index=rank,
-                                 packed=world > 1, pipeline=args.pipeline, wf_batch=args.wf_batch)
+                                 packed=world > 1, pipeline=args.pipeline, wf_batch=args.wf_batch, lean=lean)
+    p_count = dataclasses.replace(p, lean=False)
     n_out = p.output_pixels()
     fb = torch.zeros((n_out, 4), dtype=torch.float32, device=dev)
     scene.reserve(p)
@@ -153,6 +160,10 @@ def main():
         if gatherer is not None:
             gatherer.gather(fb)   # RCCL gather of the packed tile buffers + unpermute on rank 0
 
+    scene.stats()
+    scene.render_device(p_count, fb.data_ptr(), stream.cuda_stream)   # untimed counting render
+    torch.cuda.synchronize(dev)
+    counts = scene.stats()
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -175,6 +186,12 @@ def main():
     st = scene.stats()   # waits for the recorded HIP events of each path-kernel launch
 
     rays = st["rays"]
+    # per-render node/leaf/triangle counts: the counting render's (identical for a lean one)
+    renders = max(st["renders"], 1)
+    for k in ("inner_visits", "leaf_visits", "leaf_refs", "tri_tests"):
+        if lean:
+            st[k] = counts[k] * renders
+    counts_match = counts["rays"] * renders == st["rays"] and counts["shades"] * renders == st["shades"]
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -210,6 +227,9 @@ def main():
             "rays_per_step": rays // args.steps,
             "rays_per_path": round(st["rays"] / max(st["paths"], 1), 4),
             "stack_spills_per_ray": round(st["stack_spills"] / max(st["rays"], 1), 4),
+            "timed_kernel": "lean megakernel (traversal counters compiled out)" if lean else "counting",
+            "counts_source": ("untimed counting render of the same frame; rays and shades equal the timed "
+                              f"renders': {counts_match}") if lean else "timed renders",
             "kernel_ms_avg": round(kern_ms, 3),
             "gpu_ms_per_step_event": round(ev0.elapsed_time(ev1) / args.steps, 3),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

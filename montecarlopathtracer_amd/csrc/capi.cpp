@@ -369,6 +369,7 @@ Plan make_plan(const mcpt_scene& s, const mcpt_render_params* p) {
     k.tail_units = k.total_units;         // no tail split unless prepare_workspace sets one
     k.total_items = k.total_units;
     k.max_depth = p->max_depth;
+    k.lean = p->lean ? 1 : 0;
     k.illum = p->illum;
     const float a = p->fov_deg * 3.14159265359f / 360;   // CUTracer.cu:189,202
     k.tan_half_fov = static_cast<float>(std::tan(static_cast<double>(a)));

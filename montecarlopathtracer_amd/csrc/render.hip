@@ -46,7 +46,7 @@ __device__ __forceinline__ void store_part(const KernelParams& kp, uint32_t id, 
         kp.partial[id] = val;
 }
 
-template <bool IN_LDS, int S, int BLOCK, bool DBG, bool QE>
+template <bool IN_LDS, int S, int BLOCK, bool DBG, bool QE, bool COUNT>
 __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = (int)threadIdx.x;
@@ -195,7 +195,7 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
             }
 #endif
             if (mode == kTrav) {
-                if (trav_iter<S, !IN_LDS>(r, tris, nodes, leafs, st, BLOCK, spill, spill_stride, c MCPT_LU_ARG, pairs))
+                if (trav_iter<S, !IN_LDS, COUNT>(r, tris, nodes, leafs, st, BLOCK, spill, spill_stride, c MCPT_LU_ARG, pairs))
                     mode = kReady;
             }
             const uint64_t trv = __ballot(mode == kTrav);
@@ -382,8 +382,12 @@ __global__ void __launch_bounds__(256) reduce_kernel(const KernelParams kp, floa
 template <bool IN_LDS, int S, int BLOCK>
 hipError_t launch_path(const KernelParams& kp, int grid, size_t lds, hipStream_t st) {
     const bool qe = kp.mode == kModeQE;
-    auto kern = kp.unit_counters ? (qe ? path_kernel<IN_LDS, S, BLOCK, true, true> : path_kernel<IN_LDS, S, BLOCK, true, false>)
-                                 : (qe ? path_kernel<IN_LDS, S, BLOCK, false, true> : path_kernel<IN_LDS, S, BLOCK, false, false>);
+    auto kern = kp.unit_counters
+                    ? (qe ? path_kernel<IN_LDS, S, BLOCK, true, true, true> : path_kernel<IN_LDS, S, BLOCK, true, false, true>)
+                : kp.lean ? (qe ? path_kernel<IN_LDS, S, BLOCK, false, true, false>
+                                : path_kernel<IN_LDS, S, BLOCK, false, false, false>)
+                          : (qe ? path_kernel<IN_LDS, S, BLOCK, false, true, true>
+                                : path_kernel<IN_LDS, S, BLOCK, false, false, true>);
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;

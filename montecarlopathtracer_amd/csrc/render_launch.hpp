@@ -91,6 +91,7 @@ struct KernelParams {
     uint32_t lds_stack_off;              // LDS offset of the stack arrays
     uint32_t* unit_counters;             // optional [total_units][4]: rays, inner, leaf, tests
     int32_t ready_thresh;                // lanes ready before a shading round (1..64)
+    int32_t lean;                        // 1: no per-step traversal counters (mcpt_render_params::lean)
     FastDiv div_npix, div_tt, div_tiles_x, div_tile;   // npix_local, tile^2, tiles_x, tile
     // Tail split (megakernel): units [tail_units, total_units) -- the last
     // ~6 per lane -- are handed out one sample at a time (work items

@@ -231,7 +231,8 @@ __device__ __forceinline__ bool pop_entry(RayState& r, uint4* st, int stride, ui
     return !(r.best <= r.tmin * kEpsLo);
 }
 
-template <int S, bool BOXES = false>
+// COUNT = false (lean renders): the per-step counters below are compiled out
+template <int S, bool BOXES = false, bool COUNT = true>
 __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict__ tris,
                                           const uint2* __restrict__ nodes1, const uint32_t* __restrict__ leafs,
                                           uint4* st, int stride, uint4* __restrict__ spill, uint32_t spill_stride,
@@ -246,7 +247,7 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
                 return false;
             }
             steps++;
-            c.inner++;
+            if constexpr (COUNT) c.inner++;
             MCPT_LANE_USE(desc_w, desc_l, lu);
             const uint32_t left = w0 & 0x3FFFFFFFu;
             uint4 pr, bx0, bx1;
@@ -312,7 +313,7 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
                 }
             }
         }
-        c.leaf++;
+        if constexpr (COUNT) c.leaf++;
         r.lpos = w0 & 0x3FFFFFFFu;
         r.lend = r.lpos + w1;
     }
@@ -333,21 +334,21 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
         const float4 a0 = tris[3 * k0], a1 = tris[3 * k0 + 1], a2 = tris[3 * k0 + 2];
         const float4 b0 = tris[3 * k1], b1 = tris[3 * k1 + 1], b2 = tris[3 * k1 + 2];
         MCPT_LANE_USE(tri_w, tri_l, lu);
-        c.refs++;
-        c.tests++;
+        if constexpr (COUNT) c.refs++;
+        if constexpr (COUNT) c.tests++;
         test_tri_v(r, a0, a1, a2, k0);
         if (two) {
-            c.refs++;
-            c.tests++;
+            if constexpr (COUNT) c.refs++;
+            if constexpr (COUNT) c.tests++;
             test_tri_v(r, b0, b1, b2, k1);
         }
         r.lpos += two ? 2u : 1u;
     }
 #else
     for (uint32_t i = 0; i < kTriCap && r.lpos < r.lend; i++, r.lpos++) {
-        c.refs++;
+        if constexpr (COUNT) c.refs++;
         MCPT_LANE_USE(tri_w, tri_l, lu);
-        c.tests++;
+        if constexpr (COUNT) c.tests++;
         test_tri(r, tris, leafs[r.lpos]);
     }
 #endif

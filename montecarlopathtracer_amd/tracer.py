@@ -172,6 +172,7 @@ class RenderParams:
     pipeline: str = "megakernel"      # or "wavefront" (C5): identical image, different kernels
     wf_batch: int = 0                 # wavefront paths in flight per batch, 0 = 2^27 (2^28 global scenes)
     mode: str = "cvmctracer"          # or "quinengine": rtx.hlsl path semantics (see for_quinengine)
+    lean: bool = False                # megakernel without traversal counters (same image; bench timing)
 
     @staticmethod
     def for_scene(scene_id: int, **kw) -> "RenderParams":
@@ -209,6 +210,7 @@ class RenderParams:
         if self.mode not in MODES:
             raise ValueError(f"mode must be one of {sorted(MODES)}")
         p.mode = MODES[self.mode]
+        p.lean = 1 if self.lean else 0
         return p
 
     def output_pixels(self) -> int:
