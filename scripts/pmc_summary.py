@@ -13,6 +13,13 @@ import os
 import sys
 
 MATCH = os.environ.get("KERNEL_MATCH", "path_kernel")
+# bench.py times the lean megakernel (last template argument COUNT = false) and
+# runs the counting one once, untimed: profile the lean one
+LEAN = os.environ.get("KERNEL_MATCH_LEAN", "false>(mcpt::KernelParams)")
+
+
+def _pick(name):
+    return MATCH in name and (not LEAN or name.endswith(LEAN))
 
 
 def read_counters(d):
@@ -20,7 +27,7 @@ def read_counters(d):
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                if MATCH not in row.get("Kernel_Name", ""):
+                if not _pick(row.get("Kernel_Name", "")):
                     continue
                 k = row["Counter_Name"]
                 vals.setdefault(k, {}).setdefault(row["Dispatch_Id"], 0.0)
@@ -45,7 +52,7 @@ def main(out):
     for f in glob.glob(os.path.join(out, "kt", "**", "*kernel_stats.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                if MATCH in row["Name"]:
+                if _pick(row["Name"]):
                     kstats = {"name": row["Name"], "calls": int(row["Calls"]), "avg_ns": float(row["AverageNs"])}
     d = {}
     rays = bench["rays_per_step"] if bench else None
