@@ -88,11 +88,11 @@ typedef struct {
     uint32_t wf_batch;          /* wavefront: max paths in flight per batch (160 B of device
                                    memory each), 0 = 1<<27, 1<<28 for scenes in global memory */
     int32_t mode;               /* MCPT_MODE_*: path semantics (default CVMCTracer)       */
-    int32_t lean;               /* 1: the megakernel skips its per-step traversal counters
-                                   (inner/leaf visits, leaf refs, triangle tests then read 0;
-                                   image, rays, paths, shades identical; ~4% faster).  The counts
-                                   are deterministic: a counting render of the same params
-                                   reports what a lean one did.  0 (default): count */
+    int32_t lean;               /* 1: the megakernel counts only rays (paths, shades, spills,
+                                   inner/leaf visits, leaf refs, triangle tests read 0; image and
+                                   rays identical; ~1-2% faster).  The counts are deterministic:
+                                   a counting render of the same params reports what a lean one
+                                   did.  0 (default): count everything */
 } mcpt_render_params;
 
 enum {

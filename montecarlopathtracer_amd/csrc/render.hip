@@ -116,7 +116,7 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
         }
         color = v3(1, 1, 1);
         depth = 0;
-        c.paths++;
+        if constexpr (COUNT) c.paths++;
     };
     // next query of this lane: count it, root interval (one inlined copy per phase)
     auto start_ray = [&]() {
@@ -224,7 +224,7 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
                         L = emitted(color, g, 1.0f);
                         done = true;
                     } else {
-                        c.shades++;
+                        if constexpr (COUNT) c.shades++;
                         scatter(g, sc.normals, r.htri, r.hbeta, r.hgamma, r.best, 0, sd, color, r.o, r.d);
                         depth++;
                         cont = true;
@@ -240,7 +240,7 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
                         L = emitted(color, g, kp.illum);
                         done = true;
                     } else {
-                        c.shades++;
+                        if constexpr (COUNT) c.shades++;
                         scatter(g, sc.normals, r.htri, r.hbeta, r.hgamma, r.best, kp.fresnel_kd, sd, color, r.o, r.d);
                         depth++;
                         cont = true;

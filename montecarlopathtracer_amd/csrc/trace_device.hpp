@@ -231,7 +231,7 @@ __device__ __forceinline__ bool pop_entry(RayState& r, uint4* st, int stride, ui
     return !(r.best <= r.tmin * kEpsLo);
 }
 
-// COUNT = false (lean renders): the per-step counters below are compiled out
+// COUNT = false (lean renders): the counters below are compiled out (rays stay)
 template <int S, bool BOXES = false, bool COUNT = true>
 __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict__ tris,
                                           const uint2* __restrict__ nodes1, const uint32_t* __restrict__ leafs,
@@ -290,11 +290,11 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
                     if (r.sp - r.lo == S) {           // LDS part full: its oldest entry (same slot) to memory
                         spill[(uint32_t)r.lo * spill_stride] = *slot;
                         r.lo++;
-                        c.spills++;
+                        if constexpr (COUNT) c.spills++;
                     }
                 } else if (r.sp >= S) {
                     spill[(uint32_t)(r.sp - S) * spill_stride] = *slot;
-                    c.spills++;
+                    if constexpr (COUNT) c.spills++;
                 }
                 *slot = make_uint4(f0, f1, __float_as_uint(plo), __float_as_uint(r.tmax));
                 r.sp++;

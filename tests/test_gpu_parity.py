@@ -265,15 +265,13 @@ def test_seed_table_matches_in_kernel_seeding(mcpt, oracle_mod, monkeypatch, mod
 
 @pytest.mark.parametrize("sc", ["scene01", "cornell_bunny70k"])
 def test_lean_megakernel_same_image(mcpt, sc):
-    """lean=True (the bench's timed kernel) compiles the per-step traversal counters
-    out: same image, rays, paths and shades as the counting kernel; the node,
-    leaf and triangle counters read 0."""
+    """lean=True (the bench's timed kernel) compiles every counter but rays out:
+    same image and ray count as the counting kernel; the other counters read 0."""
     path = mcpt.scene_path(sc)
     scene = mcpt.Scene(mcpt.ObjModel(path))
     kw = dict(width=48, height=40, spp=6, spp_chunk=4, seed=9)
     img, st = scene.render(mcpt.RenderParams(**kw))
     img2, st2 = scene.render(mcpt.RenderParams(lean=True, **kw))
     assert np.array_equal(img, img2)
-    for k in ("rays", "paths", "shades"):
-        assert st[k] == st2[k], (k, st[k], st2[k])
-    assert st["inner_visits"] > 0 and st2["inner_visits"] == 0 and st2["tri_tests"] == 0
+    assert st["rays"] == st2["rays"]
+    assert st["inner_visits"] > 0 and st2["inner_visits"] == 0 and st2["tri_tests"] == 0 and st2["shades"] == 0
