@@ -248,6 +248,10 @@ void build_image(mcpt_scene& s) {
                          v[0] - v[6], v[1] - v[7], v[2] - v[8], 0.0f};
         std::memcpy(&rec[3], &hs.kd_prio[k], 4);
         std::memcpy(&rec[7], &hs.kd_geom[k], 4);
+        // the 2x2 minor (a-b).y (a-c).z - (a-c).y (a-b).z that Math.hpp:171-173's
+        // det() forms for both A and tM (CUTracer.cu:72-83): ray-independent, so
+        // stored once (same float operations as the kernel's, no contraction)
+        rec[11] = rec[5] * rec[10] - rec[9] * rec[6];
         std::memcpy(img + off_tris + size_t(slot) * 48, rec, 48);
     }
     // leaf references, leaves in device order

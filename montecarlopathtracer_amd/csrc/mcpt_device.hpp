@@ -222,5 +222,14 @@ __device__ __forceinline__ float det3(float m0, float m1, float m2, float m3, fl
     return res1 + res2 + res3;
 }
 
+// det3 with its last minor (m3 * m7 - m4 * m6) supplied precomputed
+__device__ __forceinline__ float det3_m(float m0, float m1, float m2, float m3, float m4, float m5,
+                                        float m6, float m7, float m8, float minor_3746) {
+    float res1 = m0 * (m4 * m8 - m5 * m7);
+    float res2 = -m1 * (m3 * m8 - m5 * m6);
+    float res3 = m2 * minor_3746;
+    return res1 + res2 + res3;
+}
+
 }  // namespace dev
 }  // namespace mcpt

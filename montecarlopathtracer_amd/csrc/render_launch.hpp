@@ -3,7 +3,8 @@
 // Scene image (one contiguous device buffer, 16-byte aligned sections; the
 // same bytes are copied verbatim into LDS by the in-LDS kernel variant):
 //   tris   3 x float4 per KD triangle: (a.xyz, brute-force rank bits),
-//          (a-b .xyz, geometry index bits), (a-c .xyz, 0)       48 B
+//          (a-b .xyz, geometry index bits), (a-c .xyz, the ray-independent
+//          minor (a-b).y (a-c).z - (a-c).y (a-b).z of det A and det tM)   48 B
 //   nodes  uint2 per KD node (BFS), stored one slot late so that every
 //          sibling pair (left, left+1; left is odd in BFS order) is one aligned
 //          16-B record: inner x = axis<<30 | left child, y = split value bits;

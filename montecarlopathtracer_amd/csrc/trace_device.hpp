@@ -103,10 +103,11 @@ __device__ __forceinline__ bool begin_ray(RayState& r, const GpuScene& sc, float
 // or t < best (2^-20 margins cover every rounding of the exact path).
 __device__ __forceinline__ void test_tri_v(RayState& r, const float4 A0, const float4 A1, const float4 A2, uint32_t k) {
     const float aox = A0.x - r.o.x, aoy = A0.y - r.o.y, aoz = A0.z - r.o.z;
-    const float detA = det3(A1.x, A2.x, r.d.x, A1.y, A2.y, r.d.y, A1.z, A2.z, r.d.z);
+    // A2.w = A1.y * A2.z - A2.y * A1.z, precomputed (the last minor of det A and det tM)
+    const float detA = det3_m(A1.x, A2.x, r.d.x, A1.y, A2.y, r.d.y, A1.z, A2.z, r.d.z, A2.w);
     const float qb = det3(aox, A2.x, r.d.x, aoy, A2.y, r.d.y, aoz, A2.z, r.d.z);
     const float qg = det3(A1.x, aox, r.d.x, A1.y, aoy, r.d.y, A1.z, aoz, r.d.z);
-    const float qt = det3(A1.x, A2.x, aox, A1.y, A2.y, aoy, A1.z, A2.z, aoz);
+    const float qt = det3_m(A1.x, A2.x, aox, A1.y, A2.y, aoy, A1.z, A2.z, aoz, A2.w);
     // sign-normalised numerators: beta, gamma, t > 0 needs all three > 0 (a NaN
     // anywhere means no hit, so min3 may drop it); detA == 0 fails the magnitude test
     const uint32_t sA = __float_as_uint(detA) & 0x80000000u;
