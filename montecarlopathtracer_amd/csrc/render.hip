@@ -4,12 +4,16 @@
 // pixel, brute-force intersect :44-96) with:
 //   * persistent workgroups (one 1024-thread workgroup per CU when the scene
 //     image fits in LDS) that pull work units (pixel, sample-chunk) from a
-//     device counter, one atomic per wave per refill (__ballot / popcount);
+//     device counter, one atomic per wave per 64 units (__ballot / popcount);
 //   * path regeneration: a lane whose path ends immediately starts the next
-//     sample of its unit, so every lane traces one ray per loop iteration;
+//     sample of its unit; traversal bursts alternate with shading rounds
+//     (raised wave priority) for the lanes whose closest hit is known;
 //   * the scene image (triangles, KD nodes, leaf ids, materials) copied into
-//     LDS once per workgroup; the KD traversal stack keeps its top S entries in
-//     LDS (lane-strided, conflict-free) and spills deeper ones to global memory;
+//     LDS once per workgroup; the KD traversal stack keeps up to S entries in
+//     LDS (lane-strided, conflict-free, managed lazily) and older ones in
+//     global memory;
+//   * RNG seeds of every path from a full-wave pre-pass (seed_kernel), the
+//     next sample's seed prefetched while a path traces;
 //   * ordered front-to-back KD traversal (split-plane intervals, conservative
 //     2^-12 margins) returning the brute-force closest hit (ties broken in the
 //     brute-force loop order), see DESIGN.md;

@@ -136,12 +136,13 @@ __device__ __forceinline__ void test_tri(RayState& r, const float4* __restrict__
     test_tri_v(r, tris[3 * k], tris[3 * k + 1], tris[3 * k + 2], k);
 }
 
-// One resumable traversal iteration: descend to a leaf, test it, pop.
-// Returns true when the ray's closest hit is final.  The children of the
-// current node are read as one 16-B sibling-pair record whose address is known
-// before the split-plane decision, so the LDS latency overlaps the decision;
-// stack entries carry the far child's record (16 B: w0, w1, lo, hi), so a pop
-// needs no node re-read.
+// One resumable traversal iteration: descend to a leaf, test it (two
+// triangles at most, both records read up front), pop (the stack top read
+// during the tests).  Returns true when the ray's closest hit is final.  The
+// children of the current node are read as one 16-B sibling-pair record whose
+// address is known before the split-plane decision, so the LDS latency overlaps
+// the decision; stack entries carry the far child's record (16 B: w0, w1, lo,
+// hi), so a pop needs no node re-read.
 #ifdef MCPT_PHASE_TIMING
 #define MCPT_LU_PARAM , LaneUse& lu
 #define MCPT_LU_ARG , lu
