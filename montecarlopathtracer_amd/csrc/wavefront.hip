@@ -243,6 +243,7 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
     WF_STAMP(tm_setup);
     for (;;) {
         // ---- traversal burst until enough lanes are done ---------------------
+        __builtin_amdgcn_s_setprio(0);
         for (;;) {
 #ifdef MCPT_PHASE_TIMING
             tm_iters++;
@@ -260,6 +261,7 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
         }
         WF_STAMP(tm_trav);
         // ---- hand-off: hit record + per-material class list -----------------
+        __builtin_amdgcn_s_setprio(1);   // as the megakernel's shading rounds: short phase, raised priority
         // Settle the prefetch (issued a whole burst ago) before any store of
         // this hand-off: gfx9's vmcnt also counts stores, so any later wait on
         // the prefetch registers would wait for the stores' acknowledgements.
