@@ -404,8 +404,10 @@ Plan make_plan(const mcpt_scene& s, const mcpt_render_params* p) {
         k.key = tea16(static_cast<uint32_t>(p->seed), static_cast<uint32_t>(p->seed >> 32));
     }
     {
+        // lanes ready before a shading round: scenes in LDS 32 (sweep 16..48);
+        // scenes in global memory 40 (C4: 24 5.15, 32 5.38, 40 5.50, 48 5.39 G rays/s)
         const char* e = std::getenv("MCPT_READY_THRESH");
-        const int th = e ? std::atoi(e) : 32;
+        const int th = e ? std::atoi(e) : (s.gpu.node_boxes == 1 ? 40 : 32);
         k.ready_thresh = th < 1 ? 1 : (th > 64 ? 64 : th);
     }
     pl.out_pixels = k.packed ? size_t(npix) : size_t(p->width) * size_t(p->height);
