@@ -236,6 +236,9 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "traffic_unit": "GB per launch (HBM read+write, rocprofv3 PMC)", "traffic_source": traffic_src,
                          "bytes_model": "SURVEY 8(d): 32*nodes+4*leafrefs+48*tris+96*shades+16*px",
+                         "note": ("frac > 1: the algorithmic bytes are served from LDS (scene image) and L2 "
+                                  "(normals), not HBM -- see traffic; the kernel is bound by VALU issue and "
+                                  "lane divergence (DESIGN.md section 5)"),
                          "achieved_own_layout": round(achieved_own, 1),
                          "bytes_per_ray": round(ab["survey"] / max(per_launch["rays"], 1), 1),
                          "per_ray": {k: round(per_launch[k] / max(per_launch["rays"], 1), 3) for k in
