@@ -428,7 +428,7 @@ Plan make_plan(const mcpt_scene& s, const mcpt_render_params* p) {
 }
 
 // tail_split: the megakernel hands the last MCPT_TAIL_UNITS_PER_LANE (default
-// 6 for shards, 4 for a whole frame) units per lane of the work-unit order out one sample at a time
+// 4) units per lane of the work-unit order out one sample at a time
 // (KernelParams::tail_units).  Without it a lane's last whole unit (32 samples,
 // ~3.5 ms) set the kernel's end: at 1024 spp, rank 0 of 8 ran 64.4 ms against
 // 55.5 ideal (86%); split 2 / 4 / 6 / 8 / 12 per lane: 92 / 96 / 98 / 97 / 96%,
@@ -473,9 +473,10 @@ void prepare_workspace(mcpt_scene& s, mcpt::KernelParams& k, bool tail_split = f
         // MCPT_TAIL_UNITS: exact count (tests); MCPT_TAIL_UNITS_PER_LANE: per lane
         const char* e = std::getenv("MCPT_TAIL_UNITS_PER_LANE");
         const char* ea = std::getenv("MCPT_TAIL_UNITS");
-        // 6 per lane for shards (rank frames are short, their tails matter); a
-        // whole frame on one GPU does best with 4 (+0.3%)
-        const uint64_t per = e ? static_cast<uint64_t>(std::max(0, std::atoi(e))) : (k.shard_count > 1 ? 6 : 4);
+        // 4 per lane: a whole frame +0.3% over 6; rank 0 of 8 shards at 97.0% of
+        // ideal (6: 96.5%, 8: 95.7%, 10: 94.8%) since the seed table and the
+        // faster traversal shortened the units
+        const uint64_t per = e ? static_cast<uint64_t>(std::max(0, std::atoi(e))) : 4;
         uint64_t tail = ea ? static_cast<uint64_t>(std::max(0LL, std::atoll(ea))) : per * lanes;
         tail = std::min<uint64_t>(tail, k.total_units);
         // item indices and tail slots stay below 2^31
