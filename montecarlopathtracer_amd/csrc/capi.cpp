@@ -377,6 +377,8 @@ Plan make_plan(const mcpt_scene& s, const mcpt_render_params* p) {
     k.illum = p->illum;
     const float a = p->fov_deg * 3.14159265359f / 360;   // CUTracer.cu:189,202
     k.tan_half_fov = static_cast<float>(std::tan(static_cast<double>(a)));
+    k.h_over_w = 1.0 * static_cast<double>(static_cast<uint32_t>(p->height)) / static_cast<double>(static_cast<uint32_t>(p->width));
+    k.inv_w_pow2 = (p->width > 0 && (p->width & (p->width - 1)) == 0) ? 1.0 / static_cast<double>(p->width) : 0.0;
     k.fresnel_kd = p->fresnel_kd ? 1 : 0;
     k.prev_count = p->prev_count;
     // camera basis (CUTracer.cu:349-359)

@@ -106,6 +106,8 @@ struct KernelParams {
     // of unit u, written by seed_kernel before the path kernel (nullptr: the
     // path kernel computes TEA-16 itself)
     const uint32_t* seeds;
+    // primary rays (CUTracer.cu:202-203, double): H / W, and 2^-k when W = 2^k (else 0)
+    double h_over_w, inv_w_pow2;
 };
 
 // Wavefront pipeline workspace (wavefront.hip).  One batch = samples

@@ -378,9 +378,13 @@ __device__ __forceinline__ void primary_ray_sd(const KernelParams& kp, int px, i
     const float biasx = (float)(uint32_t)px + (rng_next(sd) * 2.0f - 1.0f);
     const float biasy = (float)(uint32_t)py + (rng_next(sd) * 2.0f - 1.0f);
     const double th = (double)kp.tan_half_fov;
-    const double W = (double)(uint32_t)kp.width, H = (double)(uint32_t)kp.height;
-    const float idx = (float)((2.0 * (double)biasx / W - 1) * th);
-    const float idy = (float)((1.0 * H / W - 2.0 * (double)biasy / W) * th);
+    const double W = (double)(uint32_t)kp.width;
+    // (2 b) / W == (2 b) * 2^-k exactly when W = 2^k; 1.0 * H / W is the host's
+    // identical IEEE double division
+    const double qx = kp.inv_w_pow2 != 0.0 ? 2.0 * (double)biasx * kp.inv_w_pow2 : 2.0 * (double)biasx / W;
+    const double qy = kp.inv_w_pow2 != 0.0 ? 2.0 * (double)biasy * kp.inv_w_pow2 : 2.0 * (double)biasy / W;
+    const float idx = (float)((qx - 1) * th);
+    const float idy = (float)((kp.h_over_w - qy) * th);
     const float idz = -1.0f;
     V3 wr;
     wr.x = kp.right[0] * idx + kp.up[0] * idy - kp.fwd[0] * idz;
