@@ -36,9 +36,39 @@ __device__ __forceinline__ V3 vscale(V3 a, float s) { return v3(a.x * s, a.y * s
 __device__ __forceinline__ V3 vadd(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
 __device__ __forceinline__ V3 vsub(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
 __device__ __forceinline__ V3 vdiv(V3 a, float s) { return v3(a.x / s, a.y / s, a.z / s); }
+// Same-denominator division, bit-identical to IEEE f32 a / d: the quotient is
+// RN_f32(a * r) with r a double reciprocal of d within ~2^-52.  A float quotient
+// that is not exact lies more than 2^-49 (relative) from every f32 rounding
+// midpoint (a - d*m is a multiple of a grid step >= 2^-49 |a| for 24-bit a, d and
+// 25-bit m, and never 0), so the double error cannot change the rounding
+// (tests/test_div_shared.py, tests/test_gpu_math.py).
+//   1: r = IEEE double 1 / d;  2: v_rcp_f64 + two Newton steps (error <= ~2^-52;
+//   0, inf, NaN reciprocals passed through, so a / 0 and a / inf keep IEEE results)
+#ifndef MCPT_SHARED_DIV
+#define MCPT_SHARED_DIV 2
+#endif
+__device__ __forceinline__ double recip_shared(float d) {
+#if MCPT_SHARED_DIV == 2
+    const double dd = (double)d;
+    const double r0 = __builtin_amdgcn_rcp(dd);
+    double e = __builtin_fma(-dd, r0, 1.0);
+    const double r1 = __builtin_fma(r0, e, r0);
+    e = __builtin_fma(-dd, r1, 1.0);
+    const double r2 = __builtin_fma(r1, e, r1);
+    return (__builtin_isfinite(r0) && r0 != 0.0) ? r2 : r0;
+#else
+    return 1.0 / (double)d;
+#endif
+}
+__device__ __forceinline__ float div_shared(float a, double r) { return (float)((double)a * r); }
+
 __device__ __forceinline__ void normalize_cu(V3& v) {   // Utils.hpp:27-34
     float len = __builtin_sqrtf(v.x * v.x + v.y * v.y + v.z * v.z);
+#if MCPT_SHARED_DIV
+    if (fabsf(len) > kFltEps) { const double r = recip_shared(len); v.x = div_shared(v.x, r); v.y = div_shared(v.y, r); v.z = div_shared(v.z, r); }
+#else
     if (fabsf(len) > kFltEps) { v.x = v.x / len; v.y = v.y / len; v.z = v.z / len; }
+#endif
 }
 // __builtin_sqrtf is correctly rounded under HIP defaults; __fsqrt_rn is NOT on gfx950
 // (measured: ~14% of inputs off by 1 ulp, tests/test_gpu_math.py).

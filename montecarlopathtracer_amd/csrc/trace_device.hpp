@@ -118,9 +118,16 @@ __device__ __forceinline__ void test_tri_v(RayState& r, const float4 A0, const f
     const float adet = fabsf(detA) * 1.00000095367431640625f;   // 1 + 2^-20
     const bool mags_ok = !(xb + xg > adet) & !(xt > r.best * adet);
     if (signs_ok & mags_ok) {
+#if MCPT_SHARED_DIV
+        const double rA = recip_shared(detA);
+        const float beta = div_shared(qb, rA);
+        const float gamma = div_shared(qg, rA);
+        const float t = div_shared(qt, rA);
+#else
         const float beta = qb / detA;
         const float gamma = qg / detA;
         const float t = qt / detA;
+#endif
         const uint32_t prio = __float_as_uint(A0.w);
         if (beta + gamma < 1.0f && beta > 0.0f && gamma > 0.0f && t > 0.0f &&
             (t < r.best || (t == r.best && prio < r.bprio))) {

@@ -25,6 +25,11 @@ __global__ void probe(int op, int n, const float* a, const float* b, float* o0, 
         case 9: o0[i] = sqrtf(x); break;
         case 10: o0[i] = __builtin_sqrtf(x); break;
         case 11: o0[i] = pow5_f(x); break;
+        case 12: o0[i] = (float)((double)x * (1.0 / (double)y)); break;
+        case 13: { const double d = (double)y, r0 = __builtin_amdgcn_rcp(d);
+                   double e = __builtin_fma(-d, r0, 1.0); const double r1 = __builtin_fma(r0, e, r0);
+                   e = __builtin_fma(-d, r1, 1.0); const double r2 = __builtin_fma(r1, e, r1);
+                   o0[i] = (float)((double)x * ((__builtin_isfinite(r0) && r0 != 0.0) ? r2 : r0)); } break;
         default: break;
     }
 }

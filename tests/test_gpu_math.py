@@ -11,6 +11,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "hip"))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.fixture(scope="module")
@@ -54,6 +55,18 @@ def test_float_div_rcp_sqrt_exact(probe):
         o, _, _ = probe(8, a, b)
         ref = (a - b) * (np.float32(1) / (b - np.float32(0.5)))
         assert np.array_equal(o.view(np.uint32), ref.view(np.uint32))
+
+
+def test_shared_div_formulas_exact(probe):
+    """ops 12 / 13: the two recip_shared variants (IEEE double 1/d; v_rcp_f64 +
+    two Newton steps) give IEEE f32 a / d bit for bit (tests/test_div_shared.py)."""
+    from test_div_shared import same_bits, shared_cases
+    a, d = shared_cases(400_000, seed=11)
+    with np.errstate(all="ignore"):
+        ref = a / d
+    for op in (12, 13):
+        o, _, _ = probe(op, a, d)
+        assert same_bits(o, ref), op
 
 
 def test_double_div_exact(probe):
