@@ -206,8 +206,11 @@ void build_image(mcpt_scene& s) {
     const uint32_t nn = static_cast<uint32_t>(hs.nodes.size());
     const uint32_t nl = static_cast<uint32_t>(hs.leaf_ids.size());
     const uint32_t ng = static_cast<uint32_t>(hs.geoms.size());
+    // the traversal's spill area holds 32 stack entries per lane (depth cap 32)
+    if (hs.kd_depth < 0 || hs.kd_depth > 32) throw mcpt::Error{MCPT_E_INVALID, "KD tree deeper than 32"};
     for (uint32_t i = 0; i < nn; ++i)
-        if (hs.nodes[i].axis && (hs.nodes[i].left % 2u) != 1u)
+        if (hs.nodes[i].axis && ((hs.nodes[i].left % 2u) != 1u || hs.nodes[i].right != hs.nodes[i].left + 1u ||
+                                 hs.nodes[i].left + 1u >= nn || hs.nodes[i].left <= i))
             throw mcpt::Error{MCPT_E_INVALID, "KD sibling pair not at an odd index"};
     auto al16 = [](size_t x) { return (x + 15u) & ~size_t(15); };
     auto al128 = [](size_t x) { return (x + 127u) & ~size_t(127); };

@@ -6,12 +6,14 @@
 // ~0.1 s.  The cache keys a file on two independent 64-bit hashes of those
 // vertex bytes (plus the builder version) and stores the flattened nodes,
 // leaf ids and depth.  A file is used only if its header, both keys, the
-// payload checksum and a structural check (child indices forward and in
-// range, leaf ranges inside the id array, ids inside the triangle count) all
-// pass -- anything else rebuilds and rewrites it, so a stale, truncated or
-// foreign file can cost time but never change or break a render.  Writes go
+// payload checksum and a structural check (valid_tree: sibling pairs in
+// range, a tree of depth <= 32 equal to the header's, leaf ranges and ids in
+// range) all pass -- anything else rebuilds and rewrites it, so a stale,
+// truncated or foreign file can cost time but never change or break a render.  Writes go
 // to a temporary file renamed into place (concurrent processes see either
 // the old file or the whole new one).
+#include <algorithm>
+#include <cstdint>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -28,6 +30,7 @@ namespace {
 constexpr uint32_t kBuilderVersion = 1;
 constexpr char kMagic[8] = {'M', 'C', 'P', 'T', 'K', 'D', 'C', '1'};
 constexpr uint32_t kNodeWords = 12;   // left right bmin[3] bmax[3] axis split leaf_begin leaf_count
+constexpr int32_t kMaxKdDepth = 32;   // build_kdtree's cap (KDTree.hpp:103-106)
 
 struct Header {
     char magic[8];
@@ -81,18 +84,38 @@ void pack(const std::vector<KdNode>& nodes, std::vector<uint32_t>& words) {
     }
 }
 
-bool valid_tree(const std::vector<uint32_t>& w, const std::vector<uint32_t>& leaf_ids, uint64_t n_tris) {
+// Structure the consumers rely on: capi.cpp device_order/build_image read
+// nodes[left + 1] as the right sibling and write node_new[left + 1]; the
+// traversal's stack spill area holds 32 entries per lane (the builder's depth
+// cap, KDTree.hpp:103-106).  So: every inner node's children are the pair
+// (left, left + 1) with left odd and both in range, every node but the root
+// has exactly one parent (a tree, no shared subtrees), the real depth equals
+// the header's and is <= 32, and leaf ranges / ids stay inside their arrays.
+// The keys and checksums are public, so a crafted file must fail here.
+bool valid_tree(const std::vector<uint32_t>& w, const std::vector<uint32_t>& leaf_ids, uint64_t n_tris,
+                int32_t depth) {
     const size_t nn = w.size() / kNodeWords;
-    if (nn == 0) return false;
+    if (nn == 0 || depth < 0 || depth > kMaxKdDepth) return false;
+    std::vector<uint8_t> parents(nn, 0);
+    std::vector<int32_t> node_depth(nn, -1);
+    node_depth[0] = 0;
+    int32_t max_depth = 0;
     for (size_t i = 0; i < nn; ++i) {
         const uint32_t* n = &w[i * kNodeWords];
         if (n[8] > 3) return false;
+        if (node_depth[i] < 0) return false;     // unreachable (children point forward: parents come first)
+        max_depth = std::max(max_depth, node_depth[i]);
         if (n[8]) {
-            if (n[0] <= i || n[0] >= nn || n[1] <= i || n[1] >= nn) return false;
+            const uint64_t L = n[0];
+            if (L <= i || (L & 1u) != 1u || uint64_t(n[1]) != L + 1 || L + 1 >= nn) return false;
+            if (parents[L]++ || parents[L + 1]++) return false;
+            node_depth[L] = node_depth[L + 1] = node_depth[i] + 1;
+            if (node_depth[i] + 1 > kMaxKdDepth) return false;
         } else if (uint64_t(n[10]) + n[11] > leaf_ids.size()) {
             return false;
         }
     }
+    if (max_depth != depth) return false;
     for (uint32_t id : leaf_ids)
         if (id >= n_tris) return false;
     return true;
@@ -111,7 +134,7 @@ bool kd_cache_load(const std::string& dir, const std::vector<float>& tv, std::ve
     bool ok = std::fread(&h, sizeof h, 1, f) == 1 && std::memcmp(h.magic, kMagic, 8) == 0 &&
               h.version == kBuilderVersion && h.node_words == kNodeWords && h.n_tris == tv.size() / 9 &&
               h.key_a == ka && h.key_b == kb && h.n_nodes > 0 && h.n_nodes < (1ull << 31) &&
-              h.n_leaf_ids < (1ull << 31) && h.depth >= 0 && h.depth <= 64;
+              h.n_leaf_ids < (1ull << 31) && h.depth >= 0 && h.depth <= kMaxKdDepth;
     if (ok) {
         w.resize(size_t(h.n_nodes) * kNodeWords);
         ids.resize(size_t(h.n_leaf_ids));
@@ -122,7 +145,7 @@ bool kd_cache_load(const std::string& dir, const std::vector<float>& tv, std::ve
     std::fclose(f);
     if (!ok) return false;
     const uint64_t ph = fnv1a(ids.data(), ids.size() * 4, fnv1a(w.data(), w.size() * 4, 0xCBF29CE484222325ull));
-    if (ph != h.payload_hash || !valid_tree(w, ids, h.n_tris)) return false;
+    if (ph != h.payload_hash || !valid_tree(w, ids, h.n_tris, h.depth)) return false;
     nodes.assign(size_t(h.n_nodes), KdNode());
     for (size_t i = 0; i < nodes.size(); ++i) {
         const uint32_t* s = &w[i * kNodeWords];

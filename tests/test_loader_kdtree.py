@@ -234,3 +234,69 @@ def test_kd_cache_roundtrip_and_rejects_bad_files(mcpt, tmp_path):
     other = mcpt.Scene(mcpt.ObjModel(mcpt.scene_path("scene01")), host_only=True, kd_cache=d)
     assert not other.cache_hit and len(os.listdir(d)) == 2
     assert other.info()["n_nodes"] != s2.info()["n_nodes"]
+
+
+def _fnv1a(data: bytes, h: int) -> int:
+    for b in data:
+        h = ((h ^ b) * 0x100000001B3) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+def test_kd_cache_rejects_crafted_files_with_valid_hashes(mcpt, tmp_path):
+    """The cache keys and the payload checksum are public (FNV-1a), so a crafted
+    file passes them; valid_tree (kd_cache.cpp) must still reject any tree the
+    consumers cannot take: a sibling pair that is not (left, left+1), a subtree
+    shared by two parents, a header depth that is not the tree's, a depth over
+    the builder's cap of 32 (the traversal's spill area holds 32 entries).  The
+    control case -- a split value changed with the checksum recomputed -- must
+    be accepted, which shows the test writes correct checksums."""
+    import struct
+    model = mcpt.ObjModel(mcpt.scene_path("scene01"))
+    d = str(tmp_path / "kd")
+    s1 = mcpt.Scene(model, host_only=True, kd_cache=d)
+    assert not s1.cache_hit
+    path = os.path.join(d, os.listdir(d)[0])
+    blob = open(path, "rb").read()
+    hdr = bytearray(blob[:72])
+    n_nodes, n_ids = struct.unpack_from("<QQ", hdr, 40)
+    depth = struct.unpack_from("<i", hdr, 56)[0]
+    w = np.frombuffer(blob[72:72 + 48 * n_nodes], dtype=np.uint32).reshape(-1, 12).copy()
+    ids = np.frombuffer(blob[72 + 48 * n_nodes:], dtype=np.uint32).copy()
+    assert ids.size == n_ids and depth == s1.info()["kd_depth"] == 20
+
+    def write(w2, depth2=depth):
+        h = bytearray(hdr)
+        struct.pack_into("<i", h, 56, depth2)
+        ph = _fnv1a(ids.tobytes(), _fnv1a(w2.tobytes(), 0xCBF29CE484222325))
+        struct.pack_into("<Q", h, 64, ph)
+        open(path, "wb").write(bytes(h) + w2.tobytes() + ids.tobytes())
+
+    def loads():
+        return mcpt.Scene(model, host_only=True, kd_cache=d).cache_hit
+
+    inner = np.nonzero(w[:, 8])[0]
+    # control: a changed split value with a correct checksum is read back
+    w2 = w.copy(); w2[0, 9] = np.float32(0.25).view(np.uint32)
+    write(w2)
+    assert loads()
+    # right child not left + 1
+    w2 = w.copy(); w2[inner[3], 1] = w2[inner[3], 0] + 2
+    write(w2)
+    assert not loads()
+    # even left index (pair straddles two records)
+    w2 = w.copy(); w2[inner[3], 0] += 1; w2[inner[3], 1] += 1
+    write(w2)
+    assert not loads()
+    # two parents share one pair (a DAG, not a tree)
+    a, b = inner[5], inner[6]
+    w2 = w.copy(); w2[b, 0:2] = w2[a, 0:2]
+    write(w2)
+    assert not loads()
+    # header depth differs from the tree's depth
+    write(w.copy(), depth + 1)
+    assert not loads()
+    # over the cap: header depth 33
+    write(w.copy(), 33)
+    assert not loads()
+    # the last state rebuilt and rewrote the file: it loads again
+    assert loads()
