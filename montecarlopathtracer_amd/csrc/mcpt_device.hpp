@@ -70,6 +70,19 @@ __device__ __forceinline__ void normalize_cu(V3& v) {   // Utils.hpp:27-34
     if (fabsf(len) > kFltEps) { v.x = v.x / len; v.y = v.y / len; v.z = v.z / len; }
 #endif
 }
+// HLSL normalize(v) = v / length(v) (the D3D definition), no epsilon guard:
+// QuinEngine's shading normal, Fresnel output and primary ray (rtx.hlsl:250,
+// 340, 395).  Division as IEEE (shared reciprocal, bit-identical); a zero
+// vector gives NaN like 0 / 0.
+__device__ __forceinline__ void normalize_hlsl(V3& v) {
+    const float len = __builtin_sqrtf(v.x * v.x + v.y * v.y + v.z * v.z);
+#if MCPT_SHARED_DIV
+    const double r = recip_shared(len);
+    v.x = div_shared(v.x, r); v.y = div_shared(v.y, r); v.z = div_shared(v.z, r);
+#else
+    v.x = v.x / len; v.y = v.y / len; v.z = v.z / len;
+#endif
+}
 // __builtin_sqrtf is correctly rounded under HIP defaults; __fsqrt_rn is NOT on gfx950
 // (measured: ~14% of inputs off by 1 ulp, tests/test_gpu_math.py).
 __device__ __forceinline__ float sqrt_rn(float x) { return __builtin_sqrtf(x); }
@@ -197,10 +210,13 @@ __device__ __forceinline__ V3 sample_hemi(uint32_t& sd, V3 n) {   // Utils.hpp:4
     }
     return out;
 }
-__device__ __forceinline__ V3 sample_phong(uint32_t& sd, V3 n, V3 in, uint32_t Ns) {   // Utils.hpp:72-95
+// Phong lobe; ns1 = the exponent's "Ns + 1" as the caller's type computes it:
+// CVMCTracer passes Ns as unsigned int, (float)(Ns + 1u) (Utils.hpp:72-76);
+// QuinEngine keeps the float, Ns + 1.0f (rtx.hlsl:253-257)
+__device__ __forceinline__ V3 sample_phong(uint32_t& sd, V3 n, V3 in, float ns1) {   // Utils.hpp:72-95
     float x = rng_next(sd);
     float y = rng_next(sd);
-    float cosT = pow_f(x, 1.0f / (float)(Ns + 1));
+    float cosT = pow_f(x, 1.0f / ns1);
     float sinT = sqrt_rn(1 - cosT * cosT);
     float phi = 2 * kPwPi * y;
     float sp, cp;
@@ -217,7 +233,11 @@ __device__ __forceinline__ V3 sample_phong(uint32_t& sd, V3 n, V3 in, uint32_t N
     }
     return vsub(in, vscale(vscale(h, dot3(in, h)), 2.0f));
 }
-__device__ __forceinline__ V3 sample_fresnel(uint32_t& sd, V3 n, V3 in, float Tr, float Ni) {   // Utils.hpp:97-137
+// Fresnel: CVMCTracer normalizes only the refracted directions (epsilon-guarded
+// Utils.hpp:27-34; Utils.hpp:97-137); QuinEngine normalizes every output, the
+// mirror and total-internal-reflection branches included (rtx.hlsl:213-251)
+template <bool QE = false>
+__device__ __forceinline__ V3 sample_fresnel(uint32_t& sd, V3 n, V3 in, float Tr, float Ni) {
     float x = rng_next(sd);
     V3 out;
     float ndoti = dot3(in, n);
@@ -226,7 +246,7 @@ __device__ __forceinline__ V3 sample_fresnel(uint32_t& sd, V3 n, V3 in, float Tr
         if (ndoti <= 0) {
             float alpha = -ndoti / Ni - sqrt_rn(1 - (1 - ndoti * ndoti) / Ni / Ni);
             out = vadd(vscale(n, alpha), vdiv(in, Ni));
-            normalize_cu(out);
+            if constexpr (!QE) normalize_cu(out);
         } else {
             float test = 1 - (1 - ndoti * ndoti) * Ni * Ni;
             if (test < 0) {
@@ -234,12 +254,13 @@ __device__ __forceinline__ V3 sample_fresnel(uint32_t& sd, V3 n, V3 in, float Tr
             } else {
                 float alpha = -ndoti * Ni + sqrt_rn(test);
                 out = vadd(vscale(n, alpha), vscale(in, Ni));
-                normalize_cu(out);
+                if constexpr (!QE) normalize_cu(out);
             }
         }
     } else {
         out = vsub(in, vscale(vscale(n, dot3(in, n)), 2.0f));
     }
+    if constexpr (QE) normalize_hlsl(out);
     return out;
 }
 

@@ -229,7 +229,7 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
                         done = true;
                     } else {
                         if constexpr (COUNT) c.shades++;
-                        scatter(g, sc.normals, r.htri, r.hbeta, r.hgamma, r.best, 0, sd, color, r.o, r.d);
+                        scatter<true>(g, sc.normals, r.htri, r.hbeta, r.hgamma, r.best, 0, sd, color, r.o, r.d);
                         depth++;
                         cont = true;
                     }

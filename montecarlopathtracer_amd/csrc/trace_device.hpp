@@ -417,19 +417,23 @@ __device__ __forceinline__ V3 emitted(V3 color, const GpuGeom& g, float illum) {
 }
 // One scatter event at a non-emitting hit (CUTracer.cu:120-160): interpolated
 // normal, BSDF sample by material, throughput update, next origin/direction.
-// n1..n3 are the hit triangle's vertex normals (fetched by the caller).
+// n1..n3 are the hit triangle's vertex normals (fetched by the caller).  QE:
+// rtx.hlsl:336-358 -- HLSL normalize of the normal, QE Fresnel (always
+// normalized), Phong with the float Ns; fresnel_kd is 0 for QE (rtx.hlsl:345).
+template <bool QE = false>
 __device__ __forceinline__ void scatter_n(const GpuGeom& g, float4 n1, float4 n2, float4 n3, float hbeta,
                                           float hgamma, float best, int32_t fresnel_kd, uint32_t& sd, V3& color,
                                           V3& o, V3& d) {
     V3 nrm = vadd(vadd(vscale(v3(n1.x, n1.y, n1.z), 1.0f - hbeta - hgamma), vscale(v3(n2.x, n2.y, n2.z), hbeta)),
                   vscale(v3(n3.x, n3.y, n3.z), hgamma));
-    normalize_cu(nrm);
+    if constexpr (QE) normalize_hlsl(nrm);
+    else normalize_cu(nrm);
     V3 dir = d;
     if (g.Tr > 0) {
-        dir = sample_fresnel(sd, nrm, dir, g.Tr, g.Ni);
+        dir = sample_fresnel<QE>(sd, nrm, dir, g.Tr, g.Ni);
         if (fresnel_kd) color = v3(color.x * g.Kd[0], color.y * g.Kd[1], color.z * g.Kd[2]);
     } else if (g.Ns > 1) {
-        dir = sample_phong(sd, nrm, dir, g.Ns_u);
+        dir = sample_phong(sd, nrm, dir, QE ? g.Ns + 1.0f : (float)(g.Ns_u + 1u));
         color = v3(color.x * g.Ks[0], color.y * g.Ks[1], color.z * g.Ks[2]);
     } else {
         color = v3(color.x * g.Kd[0], color.y * g.Kd[1], color.z * g.Kd[2]);
@@ -444,11 +448,12 @@ __device__ __forceinline__ void scatter_n(const GpuGeom& g, float4 n1, float4 n2
     o = vadd(hp, vscale(dir, 0.01f));
     d = dir;
 }
+template <bool QE = false>
 __device__ __forceinline__ void scatter(const GpuGeom& g, const float4* __restrict__ normals, int32_t htri,
                                         float hbeta, float hgamma, float best, int32_t fresnel_kd, uint32_t& sd,
                                         V3& color, V3& o, V3& d) {
     const float4 n1 = normals[3 * htri], n2 = normals[3 * htri + 1], n3 = normals[3 * htri + 2];
-    scatter_n(g, n1, n2, n3, hbeta, hgamma, best, fresnel_kd, sd, color, o, d);
+    scatter_n<QE>(g, n1, n2, n3, hbeta, hgamma, best, fresnel_kd, sd, color, o, d);
 }
 // material class of a geometry for the wavefront's per-material queues
 __device__ __forceinline__ uint32_t material_class(const GpuGeom& g) {
@@ -535,7 +540,7 @@ __device__ __forceinline__ void primary_ray_qe_sd(const KernelParams& kp, int px
     w.y = kp.right[1] * vx + kp.up[1] * vy - kp.fwd[1] * vz;
     w.z = kp.right[2] * vx + kp.up[2] * vy - kp.fwd[2] * vz;
     o = v3(w.x + kp.eye[0], w.y + kp.eye[1], w.z + kp.eye[2]);
-    normalize_cu(w);
+    normalize_hlsl(w);   // rtx.hlsl:395 (|w| >= 1 here, so the same as the guarded form)
     dir = w;
 }
 __device__ __forceinline__ void primary_ray_qe(const KernelParams& kp, uint32_t pix, int px, int py, uint32_t s,

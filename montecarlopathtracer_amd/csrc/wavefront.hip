@@ -387,7 +387,8 @@ __global__ void __launch_bounds__(kShadeBlock) wf_shade(const KernelParams kp, c
                 c.shades++;
                 const GpuGeom& gm = geoms[__float_as_uint(tris[3 * htri + 1].w)];
                 V3 o = xyz(o4), d = xyz(d4);
-                scatter(gm, sc.normals, htri, h.y, h.z, h.x, qe ? 0 : kp.fresnel_kd, sd, color, o, d);
+                if (qe) scatter<true>(gm, sc.normals, htri, h.y, h.z, h.x, 0, sd, color, o, d);
+                else scatter<false>(gm, sc.normals, htri, h.y, h.z, h.x, kp.fresnel_kd, sd, color, o, d);
                 nr[0] = pack(o, pid);
                 nr[1] = pack(d, depth + 1u);
                 nr[2] = make_float4(0, 0, 0, 0);

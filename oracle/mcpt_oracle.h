@@ -117,6 +117,9 @@ float orc_pow5f(float x);                                        /* Fresnel (1-|
 void orc_sample_hemi(const float* n, const float* u, float* out);
 void orc_sample_phong(const float* n, const float* in, uint32_t Ns, const float* u, float* out);
 void orc_sample_fresnel(const float* n, const float* in, float Tr, float Ni, const float* u, float* out);
+/* QuinEngine samplers, rtx.hlsl:213-276: float Ns; Fresnel output always normalized */
+void orc_sample_phong_qe(const float* n, const float* in, float Ns, const float* u, float* out);
+void orc_sample_fresnel_qe(const float* n, const float* in, float Tr, float Ni, const float* u, float* out);
 float orc_tan_half_fov(float fov_deg);
 /* binary16 of x rounded toward -inf (dir < 0) / +inf (dir > 0), and back */
 uint16_t orc_f16_dir(float x, int dir);

@@ -92,6 +92,8 @@ def lib():
         L.orc_sample_hemi.argtypes = [f32p, f32p, f32p]
         L.orc_sample_phong.argtypes = [f32p, f32p, C.c_uint32, f32p, f32p]
         L.orc_sample_fresnel.argtypes = [f32p, f32p, C.c_float, C.c_float, f32p, f32p]
+        L.orc_sample_phong_qe.argtypes = [f32p, f32p, C.c_float, f32p, f32p]
+        L.orc_sample_fresnel_qe.argtypes = [f32p, f32p, C.c_float, C.c_float, f32p, f32p]
         L.orc_tan_half_fov.restype = C.c_float
         L.orc_tan_half_fov.argtypes = [C.c_float]
         L.orc_qe_proj.restype = None

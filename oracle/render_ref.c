@@ -152,6 +152,11 @@ static inline void normalize_cu(orc_v3* v) {   /* Utils.hpp:27-34 */
     float len = sqrtf(v->x * v->x + v->y * v->y + v->z * v->z);
     if (fabsf(len) > FLT_EPSILON) { v->x /= len; v->y /= len; v->z /= len; }
 }
+/* HLSL normalize(v) = v / length(v), no epsilon guard (rtx.hlsl:250, 340, 395) */
+static inline void normalize_hlsl(orc_v3* v) {
+    float len = sqrtf(v->x * v->x + v->y * v->y + v->z * v->z);
+    v->x /= len; v->y /= len; v->z /= len;
+}
 
 /* ============================== samplers =================================== */
 /* Utils.hpp:46-70 */
@@ -174,11 +179,13 @@ static orc_v3 sample_hemi(usrc* u, orc_v3 n) {
     }
     return out;
 }
-/* Utils.hpp:72-95 (Ns passed as unsigned int) */
-static orc_v3 sample_phong(usrc* u, orc_v3 n, orc_v3 in, uint32_t Ns) {
+/* Utils.hpp:72-95 / rtx.hlsl:253-276.  ns1 = "Ns + 1" in the caller's type:
+ * CVMCTracer passes Ns as unsigned int, (float)(Ns + 1u); QuinEngine keeps the
+ * float, Ns + 1.0f */
+static orc_v3 sample_phong(usrc* u, orc_v3 n, orc_v3 in, float ns1) {
     float x = next_u(u);
     float y = next_u(u);
-    float cosT = orc_powf(x, 1.0f / (float)(Ns + 1));
+    float cosT = orc_powf(x, 1.0f / ns1);
     float sinT = sqrtf(1 - cosT * cosT);
     float phi = 2 * PW_PI * y;
     orc_v3 h = v3(sinT * orc_cosf(phi), cosT, sinT * orc_sinf(phi));
@@ -193,8 +200,10 @@ static orc_v3 sample_phong(usrc* u, orc_v3 n, orc_v3 in, uint32_t Ns) {
     }
     return vsub(in, vscale(vscale(h, dot3(in, h)), 2));
 }
-/* Utils.hpp:97-137 */
-static orc_v3 sample_fresnel(usrc* u, orc_v3 n, orc_v3 in, float Tr, float Ni) {
+/* Utils.hpp:97-137 (qe = 0): only the refracted directions are normalized
+ * (epsilon-guarded); rtx.hlsl:213-251 (qe = 1): every output goes through
+ * HLSL normalize, the mirror and total-internal-reflection branches included */
+static orc_v3 sample_fresnel(usrc* u, orc_v3 n, orc_v3 in, float Tr, float Ni, int qe) {
     float x = next_u(u);
     orc_v3 out;
     float ndoti = dot3(in, n);
@@ -203,7 +212,7 @@ static orc_v3 sample_fresnel(usrc* u, orc_v3 n, orc_v3 in, float Tr, float Ni) {
         if (ndoti <= 0) {
             float alpha = -ndoti / Ni - sqrtf(1 - (1 - ndoti * ndoti) / Ni / Ni);
             out = vadd(vscale(n, alpha), vdiv(in, Ni));
-            normalize_cu(&out);
+            if (!qe) normalize_cu(&out);
         } else {
             float test = 1 - (1 - ndoti * ndoti) * Ni * Ni;
             if (test < 0) {
@@ -211,12 +220,13 @@ static orc_v3 sample_fresnel(usrc* u, orc_v3 n, orc_v3 in, float Tr, float Ni) {
             } else {
                 float alpha = -ndoti * Ni + sqrtf(test);
                 out = vadd(vscale(n, alpha), vscale(in, Ni));
-                normalize_cu(&out);
+                if (!qe) normalize_cu(&out);
             }
         }
     } else {
         out = vsub(in, vscale(vscale(n, dot3(in, n)), 2));
     }
+    if (qe) normalize_hlsl(&out);
     return out;
 }
 
@@ -227,12 +237,23 @@ void orc_sample_hemi(const float* n, const float* u, float* out) {
 }
 void orc_sample_phong(const float* n, const float* in, uint32_t Ns, const float* u, float* out) {
     usrc s = {0, u, 0};
-    orc_v3 r = sample_phong(&s, v3(n[0], n[1], n[2]), v3(in[0], in[1], in[2]), Ns);
+    orc_v3 r = sample_phong(&s, v3(n[0], n[1], n[2]), v3(in[0], in[1], in[2]), (float)(Ns + 1u));
     out[0] = r.x; out[1] = r.y; out[2] = r.z;
 }
 void orc_sample_fresnel(const float* n, const float* in, float Tr, float Ni, const float* u, float* out) {
     usrc s = {0, u, 0};
-    orc_v3 r = sample_fresnel(&s, v3(n[0], n[1], n[2]), v3(in[0], in[1], in[2]), Tr, Ni);
+    orc_v3 r = sample_fresnel(&s, v3(n[0], n[1], n[2]), v3(in[0], in[1], in[2]), Tr, Ni, 0);
+    out[0] = r.x; out[1] = r.y; out[2] = r.z;
+}
+/* QuinEngine samplers (rtx.hlsl:213-276): float Ns, normalized Fresnel output */
+void orc_sample_phong_qe(const float* n, const float* in, float Ns, const float* u, float* out) {
+    usrc s = {0, u, 0};
+    orc_v3 r = sample_phong(&s, v3(n[0], n[1], n[2]), v3(in[0], in[1], in[2]), Ns + 1.0f);
+    out[0] = r.x; out[1] = r.y; out[2] = r.z;
+}
+void orc_sample_fresnel_qe(const float* n, const float* in, float Tr, float Ni, const float* u, float* out) {
+    usrc s = {0, u, 0};
+    orc_v3 r = sample_fresnel(&s, v3(n[0], n[1], n[2]), v3(in[0], in[1], in[2]), Tr, Ni, 1);
     out[0] = r.x; out[1] = r.y; out[2] = r.z;
 }
 
@@ -595,11 +616,11 @@ static orc_v3 sample_mc(qctx* q, usrc* u, orc_v3 pos, orc_v3 dir, int max_depth,
         orc_v3 normal = vadd(vadd(vscale(n1, 1.0f - hit.beta - hit.gamma), vscale(n2, hit.beta)), vscale(n3, hit.gamma));
         normalize_cu(&normal);
         if (g->Tr > 0) {
-            dir = sample_fresnel(u, normal, dir, g->Tr, g->Ni);
+            dir = sample_fresnel(u, normal, dir, g->Tr, g->Ni, 0);
             if (fresnel_kd) { color.x *= g->Kd.x; color.y *= g->Kd.y; color.z *= g->Kd.z; }
             pos = vadd(hit.hp, vscale(dir, 0.01f));
         } else if (g->Ns > 1) {
-            dir = sample_phong(u, normal, dir, (uint32_t)g->Ns);
+            dir = sample_phong(u, normal, dir, (float)((uint32_t)g->Ns + 1u));
             color.x *= g->Ks.x; color.y *= g->Ks.y; color.z *= g->Ks.z;
             pos = vadd(hit.hp, vscale(dir, 0.01f));
         } else {
@@ -654,11 +675,11 @@ static orc_v3 sample_mc_qe(qctx* q, usrc* u, orc_v3 pos, orc_v3 dir, int depth_l
         orc_v3 n2 = s->model.normals[t->n[1]];
         orc_v3 n3 = s->model.normals[t->n[2]];
         orc_v3 normal = vadd(vadd(vscale(n1, 1.0f - hit.beta - hit.gamma), vscale(n2, hit.beta)), vscale(n3, hit.gamma));
-        normalize_cu(&normal);
+        normalize_hlsl(&normal);                              /* :340 */
         if (g->Tr > 0) {                                      /* :341-345, no Kd tint */
-            dir = sample_fresnel(u, normal, dir, g->Tr, g->Ni);
+            dir = sample_fresnel(u, normal, dir, g->Tr, g->Ni, 1);
         } else if (g->Ns > 1) {
-            dir = sample_phong(u, normal, dir, (uint32_t)g->Ns);
+            dir = sample_phong(u, normal, dir, g->Ns + 1.0f);
             color.x *= g->Ks.x; color.y *= g->Ks.y; color.z *= g->Ks.z;
         } else {
             color.x *= g->Kd.x; color.y *= g->Kd.y; color.z *= g->Kd.z;
@@ -694,7 +715,7 @@ static void qe_primary(const orc_params* p, uint32_t pix, int x, int y, uint32_t
     w.y = p->right[1] * vx + p->up[1] * vy - p->fwd[1] * vz;
     w.z = p->right[2] * vx + p->up[2] * vy - p->fwd[2] * vz;
     *o = v3(w.x + p->eye[0], w.y + p->eye[1], w.z + p->eye[2]);
-    normalize_cu(&w);
+    normalize_hlsl(&w);                                       /* :395 */
     *d = w;
 }
 

@@ -127,6 +127,61 @@ def test_samplers_rotate_into_normal_frame(oracle_mod):
         assert np.allclose(np.array(out), refl, atol=1e-5)                       # Tr=0 -> mirror
 
 
+def test_quinengine_samplers_follow_rtx_hlsl(oracle_mod):
+    """QE samplers (rtx.hlsl:213-276) against the CVMCTracer ones (Utils.hpp:72-137)
+    on injected uniforms: the Fresnel output is always HLSL-normalized (mirror
+    and total-internal-reflection branches included, rtx.hlsl:250), the refracted
+    branches agree bit for bit with CV's guarded normalize; Phong takes Ns as a
+    float (rtx.hlsl:253-257), so a non-integer Ns differs from CV's truncated one
+    and an integral one is identical."""
+    import ctypes as C
+    L = oracle_mod.lib()
+    f3 = C.c_float * 3
+    r = np.random.default_rng(5)
+
+    def hlsl_normalize(v):
+        v = v.astype(np.float32)
+        ln = np.sqrt(np.float32(v[0] * v[0] + v[1] * v[1]) + np.float32(v[2] * v[2]))
+        return (v / ln).astype(np.float32)
+
+    branches = {"reflect": 0, "tir": 0, "refract_in": 0, "refract_out": 0}
+    differ = 0
+    for _ in range(3000):
+        nv = r.standard_normal(3); nv = (nv / np.linalg.norm(nv)).astype(np.float32)
+        ind = r.standard_normal(3); ind = (ind / np.linalg.norm(ind)).astype(np.float32)
+        ndoti = float(np.dot(ind, nv))
+        x = float(r.random())
+        Tr, Ni = 0.9, 1.5
+        cv, qe = f3(), f3()
+        L.orc_sample_fresnel(f3(*nv), f3(*ind), Tr, Ni, (C.c_float * 1)(x), cv)
+        L.orc_sample_fresnel_qe(f3(*nv), f3(*ind), Tr, Ni, (C.c_float * 1)(x), qe)
+        cv, qe = np.array(cv, np.float32), np.array(qe, np.float32)
+        trp = np.float32(Tr) * (1 - L.orc_pow5f(1 - abs(ndoti)))
+        tir = ndoti > 0 and 1 - (1 - ndoti * ndoti) * Ni * Ni < 0
+        if x < trp and not tir:
+            branches["refract_in" if ndoti <= 0 else "refract_out"] += 1
+            assert np.array_equal(cv.view(np.uint32), qe.view(np.uint32))
+        else:
+            branches["tir" if x < trp else "reflect"] += 1
+            assert np.array_equal(qe.view(np.uint32), hlsl_normalize(cv).view(np.uint32))
+            differ += not np.array_equal(cv.view(np.uint32), qe.view(np.uint32))
+    assert min(branches.values()) > 20, branches
+    assert differ > 100, differ            # normalizing a mirror direction moves its last bits
+    # Phong: float Ns vs unsigned Ns
+    moved = 0
+    for _ in range(500):
+        nv = r.standard_normal(3); nv = (nv / np.linalg.norm(nv)).astype(np.float32)
+        ind = r.standard_normal(3); ind = (ind / np.linalg.norm(ind)).astype(np.float32)
+        u = (C.c_float * 2)(*r.random(2).astype(np.float32))
+        a, b, c = f3(), f3(), f3()
+        L.orc_sample_phong(f3(*nv), f3(*ind), 10, u, a)
+        L.orc_sample_phong_qe(f3(*nv), f3(*ind), 10.0, u, b)
+        assert list(a) == list(b)          # integral Ns: the same exponent 1/11
+        L.orc_sample_phong_qe(f3(*nv), f3(*ind), 10.5, u, c)
+        moved += list(a) != list(c)        # CV would truncate 10.5 to 10
+    assert moved > 450, moved
+
+
 def test_transcendentals_close_to_libm(oracle_mod):
     L = oracle_mod.lib()
     x = np.linspace(0, 2 * np.pi, 5001).astype(np.float32)
