@@ -134,6 +134,10 @@ void orc_camera_basis(const float* eye, const float* dir, const float* up,
 void orc_intersect_batch(const orc_scene* s, int traversal, int64_t n,
                          const float* o, const float* d, int32_t* tri_out,
                          int32_t* geom_out, float* hit_out, orc_counters* c);
+/* same with the ordered walk's fp16 child-box cull (node_boxes) and pthreads */
+void orc_intersect_batch_mt(const orc_scene* s, int traversal, int node_boxes, int threads, int64_t n,
+                            const float* o, const float* d, int32_t* tri_out, int32_t* geom_out, float* hit_out,
+                            orc_counters* c);
 
 /* render region; out is W*H*3 floats (only region written); if prev_count>0
  * out holds the previous running mean and is updated in place            */

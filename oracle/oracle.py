@@ -100,6 +100,8 @@ def lib():
         L.orc_qe_proj.argtypes = [C.c_float, C.c_int32, C.c_int32, f32p, f32p]
         L.orc_camera_basis.argtypes = [f32p] * 6
         L.orc_intersect_batch.argtypes = [vp, C.c_int, C.c_int64, f32p, f32p, i32p, i32p, f32p, C.POINTER(Counters)]
+        L.orc_intersect_batch_mt.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int64, f32p, f32p, i32p, i32p, f32p,
+                                             C.POINTER(Counters)]
         L.orc_render.restype = C.c_int
         L.orc_render.argtypes = [vp, C.POINTER(Params), f32p, C.POINTER(Counters)]
         _lib = L
@@ -163,19 +165,25 @@ class Scene:
     def kd_nodes(self):
         a = np.zeros((self.nnodes, 12), np.uint32); lib().orc_copy_kd_nodes(self._h, _p(a, C.c_uint32)); return a
 
+    def kd_verts(self):
+        """(n_kd, 3, 3) float32 vertex positions of the KD triangles (kd id order)"""
+        v, t = self.vertices(), self.triangles()
+        return v[t[self.kd_tris()][:, :3]].astype(np.float32)
+
     def kd_leaf_ids(self):
         a = np.zeros(max(self.nleaf_ids, 1), np.uint32); lib().orc_copy_kd_leaf_ids(self._h, _p(a, C.c_uint32))
         return a[: self.nleaf_ids]
 
     # --- queries ----------------------------------------------------------
-    def intersect(self, o, d, traversal=BRUTE):
+    def intersect(self, o, d, traversal=BRUTE, node_boxes=0, threads=1):
+        """closest hits: (kd triangle id or -1, geometry, (beta, gamma, t, hit point) x6 floats, counters)"""
         o = np.ascontiguousarray(o, np.float32).reshape(-1, 3)
         d = np.ascontiguousarray(d, np.float32).reshape(-1, 3)
         n = o.shape[0]
         tri = np.zeros(n, np.int32); geom = np.zeros(n, np.int32); hit = np.zeros((n, 6), np.float32)
         c = Counters()
-        lib().orc_intersect_batch(self._h, traversal, n, _p(o, C.c_float), _p(d, C.c_float),
-                                  _p(tri, C.c_int32), _p(geom, C.c_int32), _p(hit, C.c_float), C.byref(c))
+        lib().orc_intersect_batch_mt(self._h, traversal, node_boxes, threads, n, _p(o, C.c_float), _p(d, C.c_float),
+                                     _p(tri, C.c_int32), _p(geom, C.c_int32), _p(hit, C.c_float), C.byref(c))
         return tri, geom, hit, c.as_dict()
 
     def render(self, params: "RenderParams", out=None):

@@ -592,6 +592,76 @@ void orc_intersect_batch(const orc_scene* s, int traversal, int64_t n,
     if (c) *c = q.c;
 }
 
+/* Same, with the ordered walk's fp16 child-box cull selectable and the rays
+ * split into contiguous ranges over `threads` pthreads (test infrastructure:
+ * brute force over a 70k-triangle mesh takes ~1 ms per ray on one core). */
+typedef struct {
+    const orc_scene* s;
+    const orc_v3 (*kv)[3];
+    int traversal, node_boxes;
+    int64_t b, e;
+    const float *o, *d;
+    int32_t *tri_out, *geom_out;
+    float* hit_out;
+    orc_counters c;
+} ibjob;
+
+static void* ib_worker(void* arg) {
+    ibjob* j = (ibjob*)arg;
+    qctx q;
+    memset(&q, 0, sizeof q);
+    q.s = j->s;
+    q.kv = j->kv;
+    q.traversal = j->traversal;
+    q.node_boxes = j->node_boxes;
+    q.best_init = FLT_MAX;
+    for (int64_t i = j->b; i < j->e; i++) {
+        hit_t h = intersect(&q, v3(j->o[3 * i], j->o[3 * i + 1], j->o[3 * i + 2]),
+                            v3(j->d[3 * i], j->d[3 * i + 1], j->d[3 * i + 2]));
+        j->tri_out[i] = h.tri;
+        j->geom_out[i] = h.geom;
+        if (j->hit_out) {
+            float* ho = j->hit_out + 6 * i;
+            if (h.tri >= 0) { ho[0] = h.beta; ho[1] = h.gamma; ho[3] = h.hp.x; ho[4] = h.hp.y; ho[5] = h.hp.z; ho[2] = h.t; }
+            else memset(ho, 0, 6 * sizeof(float));
+        }
+    }
+    j->c = q.c;
+    return NULL;
+}
+
+void orc_intersect_batch_mt(const orc_scene* s, int traversal, int node_boxes, int threads, int64_t n,
+                            const float* o, const float* d, int32_t* tri_out, int32_t* geom_out, float* hit_out,
+                            orc_counters* c) {
+    int nt = threads > 0 ? threads : 1;
+    if (nt > 256) nt = 256;
+    orc_v3(*kv)[3] = malloc(sizeof(orc_v3[3]) * (size_t)(s->nkd ? s->nkd : 1));
+    for (int k = 0; k < s->nkd; k++)
+        for (int j = 0; j < 3; j++) kv[k][j] = s->model.verts[s->model.tris[s->kd_tris[k]].v[j]];
+    ibjob jobs[256];
+    pthread_t th[256];
+    for (int t = 0; t < nt; t++) {
+        ibjob* j = &jobs[t];
+        memset(j, 0, sizeof *j);
+        j->s = s; j->kv = (const orc_v3(*)[3])kv; j->traversal = traversal; j->node_boxes = node_boxes;
+        j->b = n * t / nt; j->e = n * (t + 1) / nt;
+        j->o = o; j->d = d; j->tri_out = tri_out; j->geom_out = geom_out; j->hit_out = hit_out;
+        pthread_create(&th[t], NULL, ib_worker, j);
+    }
+    orc_counters tot;
+    memset(&tot, 0, sizeof tot);
+    for (int t = 0; t < nt; t++) {
+        pthread_join(th[t], NULL);
+        const orc_counters* q = &jobs[t].c;
+        tot.rays += q->rays; tot.paths += q->paths; tot.inner_visits += q->inner_visits;
+        tot.leaf_visits += q->leaf_visits; tot.leaf_refs += q->leaf_refs; tot.tri_tests += q->tri_tests;
+        tot.shades += q->shades;
+        if (q->stack_max > tot.stack_max) tot.stack_max = q->stack_max;
+    }
+    free(kv);
+    if (c) *c = tot;
+}
+
 /* =========================== path (CUTracer.cu:98-177) ==================== */
 static orc_v3 sample_mc(qctx* q, usrc* u, orc_v3 pos, orc_v3 dir, int max_depth, float illum, int fresnel_kd) {
     const orc_scene* s = q->s;

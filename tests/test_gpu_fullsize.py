@@ -99,3 +99,28 @@ def test_progressive_render_matches_reference_image(mcpt):
     # per-pixel: both images carry 1000-spp Monte Carlo noise (the reference's own
     # 100-vs-1000 spp RMSE is 0.031); the block means above carry the bias test
     assert rmse < 0.05, rmse
+
+
+def test_scene02_progressive_render_matches_mcdocx_figure3(mcpt):
+    """scene02 (four spherical emitters, glossy slabs Ns 5/10/20/50, served from
+    global memory with the child-box cull) through RenderScene(2)'s loop, 10 x
+    100 spp at 800x600, luminance 10: its 75x75 block means match the
+    reference's MC.docx Figure 3 (Blinn-Phong, luminance 10, 10000 spp), and the
+    Phong-model render of Figure 4 / result2step/step000009.png is rejected
+    (tests/test_brute_pins.py explains the two figures)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    from test_brute_pins import _blocks_vs_figure, load_png
+    tr = mcpt.Tracer()
+    tr.initialize([0])
+    tr.create_geometry(mcpt.ObjModel(mcpt.scene_path("scene02")))
+    host = np.zeros((600, 800, 3), np.float32)
+    tr.render_scene(2, host, num_kernels=10, samples_per_kernel=100, illum=10.0)
+    tr.destroy_geometry()
+    d3 = _blocks_vs_figure(host, load_png("mcdocx_fig3_scene2_blinn_phong.png"))
+    assert d3.size >= 30 and d3.mean() < 0.006 and d3.max() < 0.010, (d3.mean(), d3.max())
+    d4 = _blocks_vs_figure(host, load_png("mcdocx_fig4_scene2_phong.png"))
+    assert d4.max() > 0.025, d4.max()
+    step = load_png("result2_step000009.png")
+    blocks = lambda a: a.reshape(6, 100, 8, 100, 3).mean(axis=(1, 3))  # noqa: E731
+    assert np.abs(blocks(host) - blocks(step)).max() > 0.1
