@@ -9,6 +9,15 @@ as interleaved 8x8 tiles (tile t -> rank t % N); total work is fixed, so the
 scaling is strong.  value = closest-hit queries of all ranks / max-over-ranks
 wall time (Mray/s).
 
+Roofline: `achieved` = the path kernel's MEASURED HBM bytes (rocprofv3 PMC
+passes of this build and workload, run by this bench in child processes:
+FETCH_SIZE x2 + WRITE_SIZE) / its HIP-event duration; the kernel is bound by
+VALU issue, reported under roofline.valu (issue and lane fractions from the
+same passes); SURVEY.md section 8(d)'s algorithmic bytes (LDS/L2-served) are
+reported separately under roofline.algorithmic.  cpu_baseline = BASELINE
+configs[0] (C1: 512x512, 16 spp, whole frame, one thread) on the CPU oracle,
+plus the same oracle on all of this process's cores over crops of the workload.
+
 Launch:  python bench.py [--gpus 1 --steps 3 --warmup 1]
          python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
              --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
@@ -38,28 +47,90 @@ def algorithmic_bytes(st: dict, pixels: int) -> dict:
     return {"survey": survey, "own": own}
 
 
-def pmc_traffic(workload: str, pipeline: str):
-    """HBM bytes per path-kernel launch (GB) from the committed rocprofv3 PMC passes
-    (profiles/<round>/pmc_summary.json: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE,
-    scripts/profile_round.sh) when they were taken on this workload; else None."""
-    import glob
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_summary.json")), reverse=True):
-        try:
-            d = json.load(open(f))
-            bl = d.get("bench_line") or {}
-            if bl.get("config", {}).get("workload") == workload and \
-                    bl.get("config", {}).get("pipeline", "megakernel") == pipeline:
-                g = d["derived"]
-                return round(g["hbm_read_GB_corrected_x2"] + g["hbm_write_GB"], 3), os.path.relpath(f, ROOT)
-        except (OSError, ValueError, KeyError):
-            continue
-    return None, None
+def _workload_args(args) -> list:
+    return ["--scene", args.scene, "--width", str(args.width), "--height", str(args.height), "--spp", str(args.spp),
+            "--spp-chunk", str(args.spp_chunk), "--pipeline", args.pipeline, "--wf-batch", str(args.wf_batch)] + \
+        (["--counting"] if args.counting else [])
 
 
-def cpu_baseline(scene_name: str, width: int, height: int, seconds: float, threads: int) -> dict:
-    """Reference CPU path = the oracle (C restatement of CUTracer.cu + the reference
-    KD traversal rtx.hlsl:84-211, pthreads over rows) on `threads` host cores, on a
-    bounded sample of the workload: centred crops rendered until `seconds` pass."""
+def pmc_pass(args, counters: list, tag: str, timeout_s: int = 150) -> dict:
+    """One rocprofv3 PMC pass over ONE render of the same workload, in a child
+    process (MI355X_MICROARCH.md 'rocprofv3 PMC slots': one pass per counter
+    group -- FETCH_SIZE uses 3 of the 4 TCC slots, WRITE_SIZE 2).  Returns the
+    per-launch counter values of the timed path kernel, or {} if the pass fails."""
+    import shutil
+    import signal
+    import subprocess
+    import tempfile
+    if not shutil.which("rocprofv3"):
+        return {}
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    from pmc_summary import read_counters
+    out = tempfile.mkdtemp(prefix=f"mcpt_pmc_{tag}_", dir="/tmp")
+    cmd = ["rocprofv3", "--pmc", *counters, "--output-format", "csv", "-d", out, "-o", "run", "--",
+           sys.executable, os.path.abspath(__file__), "--pmc-child"] + _workload_args(args)
+    env = dict(os.environ, TMPDIR="/tmp")
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    proc = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                            start_new_session=True)
+    try:
+        proc.wait(timeout=timeout_s)
+    except subprocess.TimeoutExpired:
+        os.killpg(proc.pid, signal.SIGKILL)
+        proc.wait()
+        return {}
+    try:
+        vals = read_counters(out) if proc.returncode == 0 else {}
+    finally:
+        shutil.rmtree(out, ignore_errors=True)
+    return vals
+
+
+def live_counters(args) -> dict:
+    """HBM bytes and VALU issue of the path kernel, measured now on this build
+    (three separate passes, MI355X_MICROARCH.md HBM section: FETCH_SIZE doubled
+    on gfx950, WRITE_SIZE exact; both in KiB)."""
+    c = {}
+    for tag, counters in (("fetch", ["FETCH_SIZE"]), ("write", ["WRITE_SIZE"]),
+                          ("valu", ["SQ_INSTS_VALU", "SQ_THREAD_CYCLES_VALU", "SQ_ACTIVE_INST_VALU",
+                                    "SQ_WAVE_CYCLES", "GRBM_GUI_ACTIVE"])):
+        c.update(pmc_pass(args, counters, tag))
+    return c
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_c1(gpu_rays: int) -> dict:
+    """BASELINE.json configs[0] / BASELINE.md section 3: the whole C1 frame
+    (Cornell box 512x512, 16 spp, 7 scatters + 1 terminal query) on ONE thread
+    of the reference CPU path = the oracle (C restatement of CUTracer.cu:44-218
+    with the reference's KD walk, rtx.hlsl:84-211)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # test/bench infrastructure only
+    from montecarlopathtracer_amd.scenes import scene_path
+    oracle.build()
+    s = oracle.Scene(scene_path("scene01"))
+    p = oracle.RenderParams(width=512, height=512, spp=16, spp_chunk=32, traversal=oracle.KD_REF, threads=1)
+    t0 = time.perf_counter()
+    _, c = s.render(p)
+    dt = time.perf_counter() - t0
+    return {"config": "C1 cornell 512x512 16 spp, whole frame, 1 thread", "seconds": round(dt, 3),
+            "rays": c["rays"], "paths": c["paths"], "mray_s": round(c["rays"] / dt / 1e6, 4),
+            "mpath_s": round(c["paths"] / dt / 1e6, 4), "rays_equal_gpu_c1": c["rays"] == gpu_rays}
+
+
+def cpu_all_cores(scene_name: str, width: int, height: int, seconds: float, threads: int) -> dict:
+    """The same oracle on `threads` host cores over a bounded sample of the GPU
+    workload: centred crops rendered until `seconds` pass."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # test/bench infrastructure only
     from montecarlopathtracer_amd.scenes import scene_path
@@ -67,7 +138,7 @@ def cpu_baseline(scene_name: str, width: int, height: int, seconds: float, threa
     s = oracle.Scene(scene_path(scene_name))
     crop = 64 if threads == 1 else 256
     spp = 8
-    total_rays, total_t = 0, 0.0
+    total_rays, total_paths, total_t = 0, 0, 0.0
     runs = 0
     while total_t < seconds and runs < 1024:
         x0 = (width - crop) // 2 + (runs % 4) * 8
@@ -78,11 +149,24 @@ def cpu_baseline(scene_name: str, width: int, height: int, seconds: float, threa
         _, c = s.render(p)
         total_t += time.perf_counter() - t0
         total_rays += c["rays"]
+        total_paths += c["paths"]
         runs += 1
-    return {"value": round(total_rays / total_t / 1e6, 4), "unit": "Mray/s", "cores": threads, "kind": "port",
+    return {"value": round(total_rays / total_t / 1e6, 4), "unit": "Mray/s", "cores": threads,
+            "mpath_s": round(total_paths / total_t / 1e6, 4),
             "sample": f"{runs} x ({crop}x{crop} centred crop, {spp} spp) of {scene_name} {width}x{height}, "
-                      f"{total_rays} rays in {total_t:.1f}s, oracle traversal=KD_REF (rtx.hlsl order), "
-                      f"{threads} thread(s)"}
+                      f"{total_rays} rays in {total_t:.1f}s, {threads} thread(s)"}
+
+
+def cpu_baseline(scene_name: str, width: int, height: int, seconds: float, threads: int, gpu_c1_rays: int) -> dict:
+    c1 = cpu_c1(gpu_c1_rays)
+    allc = cpu_all_cores(scene_name, width, height, seconds, threads)
+    return {"value": c1["mray_s"], "unit": "Mray/s", "cores": 1, "kind": "port",
+            "sample": (f"{c1['config']}: {c1['rays']} rays / {c1['paths']} paths in {c1['seconds']} s "
+                       f"({c1['mpath_s']} Mpath/s); oracle = C restatement of CUTracer.cu:44-218 with the "
+                       f"reference KD walk rtx.hlsl:84-211; its ray count equals the GPU's C1 render: "
+                       f"{c1['rays_equal_gpu_c1']}"),
+            "c1": c1, "all_cores": allc, "cpu_model": cpu_model(), "nproc": os.cpu_count(),
+            "affinity_cores": host_cores()}
 
 
 def host_cores() -> int:
@@ -106,10 +190,12 @@ def main():
     ap.add_argument("--spp-chunk", type=int, default=32)
     ap.add_argument("--pipeline", choices=["megakernel", "wavefront"], default="megakernel")
     ap.add_argument("--wf-batch", type=int, default=0)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = this process's CPU share (<= 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--counting", action="store_true", help="time the counting megakernel instead of the lean one")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 PMC passes (HBM bytes, VALU issue)")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)   # one render under rocprofv3
     args = ap.parse_args()
 
     import torch
@@ -137,6 +223,14 @@ def main():
 
     scene = M.Scene(M.ObjModel(M.scene_path(args.scene)))
     scene_id = 2 if args.scene in ("scene02", "scene03") else 1
+    if args.pmc_child:   # PMC pass: exactly one render of the timed kernel, then exit
+        p = M.RenderParams.for_scene(scene_id, width=args.width, height=args.height, spp=args.spp,
+                                     spp_chunk=args.spp_chunk, tile=8, pipeline=args.pipeline, wf_batch=args.wf_batch,
+                                     lean=args.pipeline == "megakernel" and not args.counting)
+        fb = torch.zeros((p.output_pixels(), 4), dtype=torch.float32, device=dev)
+        scene.render_device(p, fb.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+        torch.cuda.synchronize(dev)
+        return
     # timed renders run the megakernel lean (no per-step traversal counters, same
     # image and ray count); the node/leaf/triangle counts of the bytes model come
     # from one untimed counting render of the same frame (they are deterministic)
@@ -185,35 +279,69 @@ def main():
     elapsed = time.perf_counter() - t0
     st = scene.stats()   # waits for the recorded HIP events of each path-kernel launch
 
-    rays = st["rays"]
     # per-render node/leaf/triangle counts: the counting render's (identical for a lean one)
     renders = max(st["renders"], 1)
     for k in ("paths", "inner_visits", "leaf_visits", "leaf_refs", "tri_tests", "shades", "stack_spills"):
         if lean:
             st[k] = counts[k] * renders
     counts_match = counts["rays"] * renders == st["rays"]
+    count_keys = ("rays", "paths", "inner_visits", "leaf_visits", "leaf_refs", "tri_tests", "shades", "stack_spills")
+    kern_ms = st["kernel_ms"] / renders
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
+        # whole-job counts (every rank's shard) and the slowest rank's time
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        agg = torch.tensor([st[k] for k in ("rays", "paths", "inner_visits", "leaf_visits", "leaf_refs",
-                                              "tri_tests", "shades")] + [st["kernel_ms"]],
-                           dtype=torch.float64, device=red_dev)
+        elapsed, kern_ms = float(t[0].item()), float(t[1].item())
+        agg = torch.tensor([st[k] for k in count_keys], dtype=torch.float64, device=red_dev)
         dist.all_reduce(agg, op=dist.ReduceOp.SUM)
-        rays = int(agg[0].item())
+        for i, k in enumerate(count_keys):
+            st[k] = int(agg[i].item())
+    rays = st["rays"]
 
     if rank == 0:
-        per_launch = {k: st[k] / max(st["renders"], 1) for k in
-                      ("rays", "inner_visits", "leaf_visits", "leaf_refs", "tri_tests", "shades")}
-        kern_ms = st["kernel_ms"] / max(st["renders"], 1)
-        ab = algorithmic_bytes(per_launch, n_out)
-        achieved = ab["survey"] / (kern_ms * 1e-3) / 1e9
-        achieved_own = ab["own"] / (kern_ms * 1e-3) / 1e9
+        per_launch = {k: st[k] / renders for k in count_keys}
+        ab = algorithmic_bytes(per_launch, args.width * args.height)
+        algo_gbs = ab["survey"] / (kern_ms * 1e-3) / 1e9
         mray = rays / elapsed / 1e6
         workload = f"cornell_{args.width}x{args.height}_{args.spp}spp" + ("" if args.scene == "scene01" else
                                                                             f"_{args.scene}")
-        # the committed PMC passes are single-GPU launches of the whole frame
-        traffic, traffic_src = pmc_traffic(workload, args.pipeline) if world == 1 else (None, None)
+        roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
+                "traffic": None, "traffic_unit": "GB of HBM read+write per path-kernel launch",
+                "source": "rocprofv3 --pmc passes of this build and workload, run by this bench"}
+        if world == 1 and not args.no_pmc:
+            # measured HBM bytes: FETCH_SIZE x2 (gfx950 streaming-read undercount) + WRITE_SIZE, KiB
+            pmc = live_counters(args)
+            if "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
+                hbm = (2.0 * pmc["FETCH_SIZE"] + pmc["WRITE_SIZE"]) * 1024.0
+                gbs = hbm / (kern_ms * 1e-3) / 1e9
+                roof.update(achieved=round(gbs, 2), frac=round(gbs / HBM_PEAK_GBS, 5), traffic=round(hbm / 1e9, 3),
+                            hbm_read_GB=round(2.0 * pmc["FETCH_SIZE"] * 1024 / 1e9, 3),
+                            hbm_write_GB=round(pmc["WRITE_SIZE"] * 1024 / 1e9, 3))
+            if pmc.get("SQ_INSTS_VALU") and pmc.get("GRBM_GUI_ACTIVE"):
+                # the resource the kernel is bound by: VALU issue.  A wave64 VALU
+                # instruction occupies its SIMD for 2 cycles (MI355X_MICROARCH.md), so
+                # capacity = CUs x 4 SIMDs x cycles / 2; cycles = GRBM_GUI_ACTIVE / 8 XCDs
+                cus = torch.cuda.get_device_properties(dev).multi_processor_count
+                cycles = pmc["GRBM_GUI_ACTIVE"] / 8.0
+                issue = pmc["SQ_INSTS_VALU"] / (cus * 4 * cycles / 2.0)
+                lanes = (pmc["SQ_THREAD_CYCLES_VALU"] / (64.0 * pmc["SQ_ACTIVE_INST_VALU"])
+                         if pmc.get("SQ_ACTIVE_INST_VALU") else None)
+                roof["valu"] = {"issue_frac": round(issue, 4),
+                                "lane_util": round(lanes, 4) if lanes is not None else None,
+                                "useful_lane_frac": round(issue * lanes, 4) if lanes is not None else None,
+                                "wave_instr_per_ray": round(pmc["SQ_INSTS_VALU"] / max(per_launch["rays"], 1), 2),
+                                "clock_GHz_under_pmc": round(cycles / (kern_ms * 1e6), 3),
+                                "formula": "SQ_INSTS_VALU / (CUs*4*cycles/2); lanes = SQ_THREAD_CYCLES_VALU / "
+                                           "(64*SQ_ACTIVE_INST_VALU)"}
+        roof["binding_resource"] = ("VALU issue and lane divergence (the scene image is LDS-resident; HBM "
+                                    "carries only seeds, spills and the framebuffer)")
+        roof["algorithmic"] = {"GBps": round(algo_gbs, 1), "bytes_per_ray": round(ab["survey"] / max(per_launch["rays"], 1), 1),
+                               "bytes_per_launch": int(ab["survey"]),
+                               "model": "SURVEY 8(d): 32*nodes+4*leafrefs+48*tris+96*shades+16*px",
+                               "served_from": "LDS (scene image) and L2 (normals), not HBM",
+                               "own_layout_GBps": round(ab["own"] / (kern_ms * 1e-3) / 1e9, 1),
+                               "per_ray": {k: round(per_launch[k] / max(per_launch["rays"], 1), 3) for k in
+                                           ("inner_visits", "leaf_visits", "leaf_refs", "tri_tests", "shades")}}
         line = {
             "metric": METRIC, "value": round(mray, 3), "unit": "Mray/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
@@ -225,6 +353,8 @@ def main():
                        (f" + {'rccl' if backend == 'nccl' else backend} gather" if world > 1 else ""), "pipeline": args.pipeline,
                        "kernel_variant": st["variant"]},
             "rays_per_step": rays // args.steps,
+            "paths_per_step": st["paths"] // args.steps,
+            "mpath_s": round(st["paths"] / elapsed / 1e6, 3),
             "rays_per_path": round(st["rays"] / max(st["paths"], 1), 4),
             "stack_spills_per_ray": round(st["stack_spills"] / max(st["rays"], 1), 4),
             "timed_kernel": "lean megakernel (traversal counters compiled out)" if lean else "counting",
@@ -232,22 +362,15 @@ def main():
                               f"renders': {counts_match}") if lean else "timed renders",
             "kernel_ms_avg": round(kern_ms, 3),
             "gpu_ms_per_step_event": round(ev0.elapsed_time(ev1) / args.steps, 3),
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "traffic_unit": "GB per launch (HBM read+write, rocprofv3 PMC)", "traffic_source": traffic_src,
-                         "bytes_model": "SURVEY 8(d): 32*nodes+4*leafrefs+48*tris+96*shades+16*px",
-                         "note": ("frac > 1: the algorithmic bytes are served from LDS (scene image) and L2 "
-                                  "(normals), not HBM -- see traffic; the kernel is bound by VALU issue and "
-                                  "lane divergence (DESIGN.md section 5)"),
-                         "achieved_own_layout": round(achieved_own, 1),
-                         "bytes_per_ray": round(ab["survey"] / max(per_launch["rays"], 1), 1),
-                         "per_ray": {k: round(per_launch[k] / max(per_launch["rays"], 1), 3) for k in
-                                     ("inner_visits", "leaf_visits", "leaf_refs", "tri_tests", "shades")}},
+            "roofline": roof,
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:
+            # the GPU's own C1 frame, for the ray-count check of the CPU run
+            s1 = scene if args.scene == "scene01" else M.Scene(M.ObjModel(M.scene_path("scene01")))
+            _, c1 = s1.render(M.RenderParams(width=512, height=512, spp=16, spp_chunk=32))
             line["cpu_baseline"] = cpu_baseline(args.scene, args.width, args.height, args.cpu_seconds,
-                                                args.cpu_threads or host_cores())
+                                                args.cpu_threads or host_cores(), c1["rays"])
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
