@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define MCPT_ABI_VERSION 3
+#define MCPT_ABI_VERSION 4
 
 enum {
     MCPT_OK = 0,
@@ -66,6 +66,7 @@ typedef struct {
     int64_t lds_bytes;     /* LDS image size; 0 if the scene is served from global memory */
     int64_t device;        /* HIP device ordinal holding the scene */
     int64_t node_boxes;    /* 1: served from global memory, children culled by their KD boxes */
+    int64_t n_devices;     /* devices holding a replica (mcpt_init's list at creation); 0 host-only */
 } mcpt_scene_info;
 
 typedef struct {
@@ -125,14 +126,22 @@ typedef struct {
     double reduce_ms;           /* summed GPU time of the partial-sum reduction */
     int32_t variant;            /* variant of the last call: megakernel 1,2 scene in LDS, 3 global;
                                    wavefront 4 scene in LDS, 5 global */
-    int32_t pad_;
+    int32_t devices;            /* devices the record covers: counters are summed over them,
+                                   kernel_ms / reduce_ms are the slowest device's */
 } mcpt_render_stats;
 
 /* ---- library ------------------------------------------------------------ */
 int mcpt_abi_version(void);
 const char* mcpt_last_error(void);
-/* Initialize: select the HIP device(s) used by later scene_create calls on this
- * thread (first entry becomes current).  n_devices == 0 keeps the current one. */
+/* Initialize (CUTracer.cu:220-223): select the HIP device(s) used by later
+ * scene_create calls on this thread; devices[0] becomes current and holds the
+ * scene.  n_devices > 1: the scene is replicated on every listed device, and
+ * each unsharded render (shard_count <= 1, packed = 0) is split into
+ * n_devices interleaved-tile shards (tile t -> device t % n), rendered
+ * concurrently, peer-copied to devices[0] (xGMI DMA) and unpermuted there --
+ * the single-device image bit for bit; stats sum the devices.  A device may
+ * be listed twice (two replicas on one GPU).  n_devices == 0 keeps the
+ * current device and a single-device scene. */
 int mcpt_init(const int32_t* devices, int32_t n_devices);
 int mcpt_device_count(int32_t* out);
 /* fill defaults = the CVMCTracer constants for scene 1 (CUTracer.cu:347-360) */

@@ -34,6 +34,14 @@ inline int Initialize() {            // CUTracer.cu:220-223: cudaSetDevice(0)
     return mcpt_init(&dev, 1);
 }
 
+// Multi-GPU extension (no reference counterpart: the reference ran on one GPU):
+// scenes created afterwards are replicated on every listed device and each
+// RenderScene launch is split into interleaved tiles across them, gathered to
+// devices[0] -- the same image as Initialize() gives (mcpt.h, mcpt_init).
+inline int Initialize(const std::vector<int32_t>& devices) {
+    return mcpt_init(devices.data(), static_cast<int32_t>(devices.size()));
+}
+
 // ObjModelT: PW::FileReader::ObjModel (ObjReader.hpp:37-63): m_vertices, m_normals
 // (x,y,z floats), m_triangles (m_vertexIndex[3], m_textureIndex[3], m_normalIndex[3],
 // materialIndex), m_materials (Ka/Kd/Ks .x .y .z, Ns, Tr, Ni), m_groups (map name ->

@@ -21,7 +21,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MCPT_LIB_PATH") or os.path.join(_HERE, "lib", "libmcpt.so")
 
 MCPT_OK = 0
-ABI_VERSION = 3
+ABI_VERSION = 4
 MODE_CVMCTRACER = 0
 MODE_QUINENGINE = 1
 PIPELINE_MEGAKERNEL = 0
@@ -43,7 +43,7 @@ class ModelInfo(C.Structure):
 class SceneInfo(C.Structure):
     _fields_ = [(n, C.c_int64) for n in
                 ("n_geometries", "n_triangles", "n_nodes", "n_leaf_refs", "kd_depth", "lds_bytes", "device",
-                 "node_boxes")]
+                 "node_boxes", "n_devices")]
 
 
 class RenderParamsC(C.Structure):
@@ -62,11 +62,11 @@ class RenderStats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in
                 ("rays", "paths", "inner_visits", "leaf_visits", "leaf_refs", "tri_tests", "shades",
                  "stack_spills", "renders")] + [
-        ("kernel_ms", C.c_double), ("reduce_ms", C.c_double), ("variant", C.c_int32), ("pad_", C.c_int32)]
+        ("kernel_ms", C.c_double), ("reduce_ms", C.c_double), ("variant", C.c_int32), ("devices", C.c_int32)]
 
     def as_dict(self):
         return {n: (getattr(self, n) if isinstance(getattr(self, n), float) else int(getattr(self, n)))
-                for n, _ in self._fields_ if n != "pad_"}
+                for n, _ in self._fields_}
 
 
 class ModelDesc(C.Structure):

@@ -29,6 +29,9 @@ struct mcpt_model {
 namespace {
 
 thread_local std::string g_err;
+// mcpt_init's device list for scenes created later on this thread (empty: the
+// current device only)
+thread_local std::vector<int> g_devices;
 
 int fail(int code, const std::string& msg) {
     g_err = msg;
@@ -112,6 +115,16 @@ struct mcpt_scene {
     std::vector<Timing> pending, free_timing;
     int last_variant = 0;
     uint64_t renders = 0;
+    // multi-device scene (mcpt_init with n > 1): the primary (this object, on
+    // devices[0]) owns one replica per further device -- the same image and
+    // normals, its own workspace, a non-blocking stream and a completion event --
+    // and the gather buffer its shards are peer-copied into
+    std::vector<std::unique_ptr<mcpt_scene>> replicas;
+    hipStream_t stream = nullptr;       // replicas: the shard's stream
+    hipEvent_t done = nullptr;          // replicas: shard rendered and copied
+    hipEvent_t start = nullptr;         // primary: inputs ready on the caller's stream
+    void* gather = nullptr;
+    size_t gather_bytes = 0;
 
     ~mcpt_scene() {
         if (!on_device) return;
@@ -119,10 +132,14 @@ struct mcpt_scene {
         (void)hipGetDevice(&prev);
         (void)hipSetDevice(device);
         (void)hipDeviceSynchronize();
-        for (void* p : {d_image, d_normals, ws.partial, ws.small, ws.spill, ws.fb, ws.wf, ws.tail, ws.seeds})
+        for (void* p : {d_image, d_normals, ws.partial, ws.small, ws.spill, ws.fb, ws.wf, ws.tail, ws.seeds, gather})
             if (p) (void)hipFree(p);
         for (auto& t : pending) for (auto ev : t.e) (void)hipEventDestroy(ev);
         for (auto& t : free_timing) for (auto ev : t.e) (void)hipEventDestroy(ev);
+        for (hipEvent_t ev : {done, start})
+            if (ev) (void)hipEventDestroy(ev);
+        if (stream) (void)hipStreamDestroy(stream);
+        replicas.clear();                 // each replica frees on its own device
         if (prev >= 0) (void)hipSetDevice(prev);
     }
 };
@@ -528,12 +545,23 @@ void set_device(const mcpt_scene& s) {
     if (cur != s.device) HIP_TRY(hipSetDevice(s.device));
 }
 
+void render_multi(mcpt_scene& s, const mcpt_render_params* p, float* d_fb, hipStream_t st);
+
+bool multi_device(const mcpt_scene& s, const mcpt_render_params* p, const uint32_t* d_unit_counters) {
+    return !s.replicas.empty() && p && p->shard_count <= 1 && !p->packed && !d_unit_counters;
+}
+
 void render_async(mcpt_scene& s, const mcpt_render_params* p, float* d_fb, hipStream_t st,
-                  uint32_t* d_unit_counters = nullptr) {
+                  uint32_t* d_unit_counters = nullptr, bool raw_mean = false) {
     if (!s.on_device) throw mcpt::Error{MCPT_E_INVALID, "scene was created host-only"};
     if (!d_fb) throw mcpt::Error{MCPT_E_INVALID, "framebuffer is NULL"};
+    if (multi_device(s, p, d_unit_counters)) {
+        render_multi(s, p, d_fb, st);
+        return;
+    }
     set_device(s);
     Plan pl = make_plan(s, p);
+    pl.kp.raw_mean = raw_mean ? 1 : 0;
     // the tail split hands units out by sample, so per-unit counters need whole units
     prepare_workspace(s, pl.kp, pl.pipeline == MCPT_PIPELINE_MEGAKERNEL && !d_unit_counters);
     pl.kp.unit_counters = d_unit_counters;
@@ -595,11 +623,100 @@ void read_stats(mcpt_scene& s, mcpt_render_stats* out) {
         r.leaf_refs = st[4]; r.tri_tests = st[5]; r.shades = st[6]; r.stack_spills = st[7];
     }
     r.renders = s.renders;
+    r.devices = 1;
     s.renders = 0;
     r.kernel_ms = kms;
     r.reduce_ms = rms;
     r.variant = s.last_variant;
     if (out) *out = r;
+}
+
+// Multi-device render (mcpt_init with n > 1; the reference's Initialize(),
+// CUTracer.cu:220-223, picked one device): shard r of n = the interleaved tiles
+// t with t % n == r (the same partition as the one-process-per-GPU bench),
+// rendered by device r into its packed means, peer-copied (xGMI DMA) into the
+// primary's gather buffer, then unpermuted there with the running mean.  The
+// RNG is keyed per (pixel, sample), so the image is the single-device one bit
+// for bit.  Cross-device order: every shard waits for `start` (recorded on the
+// caller's stream), the caller's stream waits for every shard's `done`.
+void render_multi(mcpt_scene& s, const mcpt_render_params* p, float* d_fb, hipStream_t st) {
+    set_device(s);
+    const Plan full = make_plan(s, p);                  // validates p; row-major output
+    const int n = 1 + static_cast<int>(s.replicas.size());
+    const int T = full.kp.tile;
+    const uint64_t ntiles = uint64_t(full.kp.tiles_x) * ((uint64_t(p->height) + T - 1) / T);
+    const uint64_t slot = (ntiles + n - 1) / n * uint64_t(T) * uint64_t(T);
+    if (slot * n >= (uint64_t(1) << 32)) throw mcpt::Error{MCPT_E_UNSUPPORTED, "image too large"};
+    ensure_buf(s.gather, s.gather_bytes, size_t(n) * slot * 16);
+    if (!s.start) HIP_TRY(hipEventCreateWithFlags(&s.start, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(s.start, st));
+    auto shard = [&](int r) {
+        mcpt_render_params pr = *p;
+        pr.shard_count = n;
+        pr.shard_index = r;
+        pr.packed = 1;
+        return pr;
+    };
+    for (int r = 1; r < n; ++r) {
+        mcpt_scene& R = *s.replicas[size_t(r - 1)];
+        set_device(R);
+        const mcpt_render_params pr = shard(r);
+        const size_t bytes = size_t(mcpt_shard_pixel_count(&pr)) * 16;
+        ensure_buf(R.ws.fb, R.ws.fb_bytes, bytes);
+        HIP_TRY(hipStreamWaitEvent(R.stream, s.start, 0));
+        render_async(R, &pr, static_cast<float*>(R.ws.fb), R.stream, nullptr, true);
+        char* dst = static_cast<char*>(s.gather) + size_t(r) * slot * 16;
+        if (R.device == s.device)
+            HIP_TRY(hipMemcpyAsync(dst, R.ws.fb, bytes, hipMemcpyDeviceToDevice, R.stream));
+        else
+            HIP_TRY(hipMemcpyPeerAsync(dst, s.device, R.ws.fb, R.device, bytes, R.stream));
+        HIP_TRY(hipEventRecord(R.done, R.stream));
+    }
+    set_device(s);
+    const mcpt_render_params p0 = shard(0);
+    render_async(s, &p0, static_cast<float*>(s.gather), st, nullptr, true);
+    for (auto& R : s.replicas) HIP_TRY(hipStreamWaitEvent(st, R->done, 0));
+    mcpt::GatherParams g{};
+    g.src = static_cast<const float4*>(s.gather);
+    g.fb = reinterpret_cast<float4*>(d_fb);
+    g.slot = static_cast<uint32_t>(slot);
+    g.width = p->width; g.height = p->height; g.tile = T; g.tiles_x = full.kp.tiles_x; g.nshards = n;
+    g.prev_count = p->prev_count;
+    g.mode = p->mode;
+    HIP_TRY(mcpt::launch_gather(g, st));
+}
+
+// stats of a (multi-device) scene: counters summed over devices; kernel and
+// reduce times the slowest device's (the devices run concurrently)
+void read_stats_all(mcpt_scene& s, mcpt_render_stats* out) {
+    mcpt_render_stats r;
+    read_stats(s, &r);
+    for (auto& R : s.replicas) {
+        mcpt_render_stats q;
+        read_stats(*R, &q);
+        r.rays += q.rays; r.paths += q.paths; r.inner_visits += q.inner_visits; r.leaf_visits += q.leaf_visits;
+        r.leaf_refs += q.leaf_refs; r.tri_tests += q.tri_tests; r.shades += q.shades;
+        r.stack_spills += q.stack_spills;
+        r.kernel_ms = std::max(r.kernel_ms, q.kernel_ms);
+        r.reduce_ms = std::max(r.reduce_ms, q.reduce_ms);
+    }
+    r.devices = 1 + static_cast<int32_t>(s.replicas.size());
+    set_device(s);
+    if (out) *out = r;
+}
+
+// device copies of the scene image and the shading normals on `device`
+void upload(mcpt_scene& s, int device, const std::vector<unsigned char>& image, const std::vector<float>& nrm) {
+    HIP_TRY(hipSetDevice(device));
+    s.device = device;
+    HIP_TRY(hipDeviceGetAttribute(&s.cus, hipDeviceAttributeMultiprocessorCount, s.device));
+    s.on_device = true;
+    HIP_TRY(hipMalloc(&s.d_image, image.size()));
+    HIP_TRY(hipMemcpy(s.d_image, image.data(), image.size(), hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc(&s.d_normals, nrm.size() * 4));
+    HIP_TRY(hipMemcpy(s.d_normals, nrm.data(), nrm.size() * 4, hipMemcpyHostToDevice));
+    s.gpu.image = static_cast<const unsigned char*>(s.d_image);
+    s.gpu.normals = static_cast<const float4*>(s.d_normals);
 }
 
 }  // namespace
@@ -619,6 +736,7 @@ int mcpt_init(const int32_t* devices, int32_t n) {
         for (int i = 0; i < n; ++i)
             if (devices[i] < 0 || devices[i] >= count) return fail(MCPT_E_INVALID, "device ordinal out of range");
         HIP_TRY(hipSetDevice(devices[0]));
+        g_devices.assign(devices, devices + n);
         return MCPT_OK;
     });
 }
@@ -794,21 +912,26 @@ static int scene_create_impl(const mcpt_model* m, mcpt_scene** out, bool device,
         if (s->hs.kd_tris.empty()) return fail(MCPT_E_INVALID, "scene has no triangles");
         build_image(*s);
         if (device) {
-            HIP_TRY(hipGetDevice(&s->device));
-            HIP_TRY(hipDeviceGetAttribute(&s->cus, hipDeviceAttributeMultiprocessorCount, s->device));
-            s->on_device = true;
-            HIP_TRY(hipMalloc(&s->d_image, s->image.size()));
-            HIP_TRY(hipMemcpy(s->d_image, s->image.data(), s->image.size(), hipMemcpyHostToDevice));
             const size_t nt = s->hs.kd_tris.size();
             std::vector<float> nrm(nt * 12, 0.0f);
             for (size_t k = 0; k < nt; ++k)          // image triangle order
                 for (int j = 0; j < 3; ++j)
                     for (int c = 0; c < 3; ++c)
                         nrm[12 * k + 4 * j + c] = s->hs.kd_normals[9 * size_t(s->tri_order[k]) + 3 * j + c];
-            HIP_TRY(hipMalloc(&s->d_normals, nrm.size() * 4));
-            HIP_TRY(hipMemcpy(s->d_normals, nrm.data(), nrm.size() * 4, hipMemcpyHostToDevice));
-            s->gpu.image = static_cast<const unsigned char*>(s->d_image);
-            s->gpu.normals = static_cast<const float4*>(s->d_normals);
+            int cur = 0;
+            HIP_TRY(hipGetDevice(&cur));
+            const std::vector<int> devs = g_devices.empty() ? std::vector<int>{cur} : g_devices;
+            upload(*s, devs[0], s->image, nrm);
+            // replicas for the further devices: same image, own workspace and stream
+            for (size_t i = 1; i < devs.size(); ++i) {
+                auto R = std::make_unique<mcpt_scene>();
+                R->gpu = s->gpu;
+                upload(*R, devs[i], s->image, nrm);
+                HIP_TRY(hipStreamCreateWithFlags(&R->stream, hipStreamNonBlocking));
+                HIP_TRY(hipEventCreateWithFlags(&R->done, hipEventDisableTiming));
+                s->replicas.push_back(std::move(R));
+            }
+            HIP_TRY(hipSetDevice(devs[0]));
         }
         *out = s.release();
         return MCPT_OK;
@@ -834,6 +957,7 @@ int mcpt_scene_get_info(const mcpt_scene* s, mcpt_scene_info* out) {
     out->lds_bytes = s->gpu.node_boxes ? 0 : s->gpu.image_bytes;
     out->node_boxes = s->gpu.node_boxes;
     out->device = s->device;
+    out->n_devices = s->on_device ? 1 + static_cast<int64_t>(s->replicas.size()) : 0;
     return MCPT_OK;
 }
 
@@ -874,7 +998,7 @@ int mcpt_render_device(mcpt_scene* s, const mcpt_render_params* p, float* d_fb_r
 int mcpt_render_stats_read(mcpt_scene* s, mcpt_render_stats* out) {
     return guarded([&]() -> int {
         if (!s || !s->on_device) return fail(MCPT_E_INVALID, "scene is not on a device");
-        read_stats(*s, out);
+        read_stats_all(*s, out);
         return MCPT_OK;
     });
 }
@@ -896,7 +1020,7 @@ static int render_sync(mcpt_scene* s, const mcpt_render_params* p, float* fb_rgb
         } else {
             HIP_TRY(hipMemset(s->ws.fb, 0, npx * 16));
         }
-        read_stats(*s, nullptr);   // start a fresh record
+        read_stats_all(*s, nullptr);   // start a fresh record
         void* d_uc = nullptr;
         const size_t uc_bytes = size_t(pl.kp.total_units) * 16;
         if (unit_counters) {
@@ -912,7 +1036,7 @@ static int render_sync(mcpt_scene* s, const mcpt_render_params* p, float* fb_rgb
         HIP_TRY(hipMemcpy(rgba.data(), s->ws.fb, npx * 16, hipMemcpyDeviceToHost));
         for (size_t i = 0; i < npx; ++i)
             for (int c = 0; c < 3; ++c) fb_rgb[3 * i + c] = rgba[4 * i + c];
-        read_stats(*s, stats);
+        read_stats_all(*s, stats);
         return MCPT_OK;
     });
 }
@@ -957,10 +1081,30 @@ int mcpt_shard_pixels(const mcpt_render_params* p, int32_t* xy) {
 int mcpt_scene_reserve(mcpt_scene* s, const mcpt_render_params* p) {
     return guarded([&]() -> int {
         if (!s || !s->on_device) return fail(MCPT_E_INVALID, "scene is not on a device");
+        auto reserve = [&](mcpt_scene& sc, const mcpt_render_params* q) {
+            set_device(sc);
+            Plan pl = make_plan(sc, q);
+            prepare_workspace(sc, pl.kp, pl.pipeline == MCPT_PIPELINE_MEGAKERNEL);
+            if (pl.pipeline == MCPT_PIPELINE_WAVEFRONT) (void)prepare_wavefront(sc, pl);
+        };
+        if (!multi_device(*s, p, nullptr)) {
+            reserve(*s, p);
+            return MCPT_OK;
+        }
+        const int n = 1 + static_cast<int>(s->replicas.size());
+        for (int r = 0; r < n; ++r) {
+            mcpt_render_params pr = *p;
+            pr.shard_count = n; pr.shard_index = r; pr.packed = 1;
+            mcpt_scene& sc = r ? *s->replicas[size_t(r - 1)] : *s;
+            reserve(sc, &pr);
+            if (r) ensure_buf(sc.ws.fb, sc.ws.fb_bytes, size_t(mcpt_shard_pixel_count(&pr)) * 16);
+        }
         set_device(*s);
-        Plan pl = make_plan(*s, p);
-        prepare_workspace(*s, pl.kp, pl.pipeline == MCPT_PIPELINE_MEGAKERNEL);
-        if (pl.pipeline == MCPT_PIPELINE_WAVEFRONT) (void)prepare_wavefront(*s, pl);
+        // the gather buffer: n slots of the largest shard (shard 0 owns the most tiles)
+        mcpt_render_params p0 = *p;
+        p0.shard_count = n; p0.shard_index = 0; p0.packed = 1;
+        ensure_buf(s->gather, s->gather_bytes, size_t(n) * size_t(mcpt_shard_pixel_count(&p0)) * 16);
+        if (!s->start) HIP_TRY(hipEventCreateWithFlags(&s->start, hipEventDisableTiming));
         return MCPT_OK;
     });
 }

@@ -345,6 +345,19 @@ __global__ void __launch_bounds__(256) seed_kernel(const KernelParams kp, uint4*
     }
 }
 
+// running mean of a pixel (CUTracer.cu:214-217; QE gamma-space, rtx.hlsl:401-402):
+// the old framebuffer value pv (read only when prev_count > 0) and this call's mean
+__device__ __forceinline__ float4 running_mean(float4 pv, V3 mean, uint32_t prev_count, int32_t mode) {
+    if (mode == kModeQE) {
+        if (!prev_count) pv = make_float4(0, 0, 0, 0);
+        return make_float4(qe_blend(pv.x, mean.x, prev_count), qe_blend(pv.y, mean.y, prev_count),
+                           qe_blend(pv.z, mean.z, prev_count), 0.0f);
+    }
+    if (prev_count == 0) return make_float4(mean.x, mean.y, mean.z, 0.0f);
+    const float pc = (float)prev_count, pc1 = (float)(prev_count + 1u);
+    return make_float4((pv.x * pc + mean.x) / pc1, (pv.y * pc + mean.y) / pc1, (pv.z * pc + mean.z) / pc1, 0.0f);
+}
+
 // partial sums -> mean -> running mean (CUTracer.cu:214-217), chunk order
 __global__ void __launch_bounds__(256) reduce_kernel(const KernelParams kp, float4* __restrict__ fb) {
     const uint32_t v = blockIdx.x * 256u + threadIdx.x;
@@ -368,19 +381,29 @@ __global__ void __launch_bounds__(256) reduce_kernel(const KernelParams kp, floa
     }
     const V3 mean = vdiv(sum, (float)kp.spp);
     const size_t idx = kp.packed ? (size_t)v : (size_t)y * (size_t)kp.width + (size_t)x;
-    float4 out;
-    if (kp.mode == kModeQE) {   // gamma-space running mean (rtx.hlsl:401-402)
-        const float4 pv = kp.prev_count ? fb[idx] : make_float4(0, 0, 0, 0);
-        out = make_float4(qe_blend(pv.x, mean.x, kp.prev_count), qe_blend(pv.y, mean.y, kp.prev_count),
-                          qe_blend(pv.z, mean.z, kp.prev_count), 0.0f);
-    } else if (kp.prev_count == 0) {
-        out = make_float4(mean.x, mean.y, mean.z, 0.0f);
-    } else {
-        const float4 pv = fb[idx];
-        const float pc = (float)kp.prev_count, pc1 = (float)(kp.prev_count + 1u);
-        out = make_float4((pv.x * pc + mean.x) / pc1, (pv.y * pc + mean.y) / pc1, (pv.z * pc + mean.z) / pc1, 0.0f);
+    if (kp.raw_mean) {
+        fb[idx] = make_float4(mean.x, mean.y, mean.z, 0.0f);
+        return;
     }
-    fb[idx] = out;
+    const bool old = kp.prev_count != 0;
+    fb[idx] = running_mean(old ? fb[idx] : make_float4(0, 0, 0, 0), mean, kp.prev_count, kp.mode);
+}
+
+// multi-device gather: shard r's packed means -> row-major running mean
+__global__ void __launch_bounds__(256) gather_kernel(const GatherParams g) {
+    const uint32_t v = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t r = blockIdx.y;
+    if (v >= g.slot) return;
+    const uint32_t T = (uint32_t)g.tile, T2 = T * T;
+    const uint32_t k = v / T2, w = v - k * T2;
+    const uint64_t t = (uint64_t)r + (uint64_t)k * (uint32_t)g.nshards;
+    const uint32_t tx = (uint32_t)(t % (uint32_t)g.tiles_x), ty = (uint32_t)(t / (uint32_t)g.tiles_x);
+    const uint32_t x = tx * T + w % T, y = ty * T + w / T;
+    if (x >= (uint32_t)g.width || y >= (uint32_t)g.height) return;   // also t past the last tile
+    const float4 m = g.src[(size_t)r * g.slot + v];
+    const size_t idx = (size_t)y * (size_t)g.width + x;
+    g.fb[idx] = running_mean(g.prev_count ? g.fb[idx] : make_float4(0, 0, 0, 0), v3(m.x, m.y, m.z), g.prev_count,
+                             g.mode);
 }
 
 template <bool IN_LDS, int S, int BLOCK>
@@ -451,6 +474,12 @@ void read_lane_use(unsigned long long out[6]) {   // megakernel lane-use counter
 
 hipError_t launch_reduce(const KernelParams& kp, float4* fb, hipStream_t st) {
     hipLaunchKernelGGL(reduce_kernel, dim3((kp.npix_local + 255u) / 256u), dim3(256), 0, st, kp, fb);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather(const GatherParams& g, hipStream_t st) {
+    if (!g.slot || g.nshards < 1) return hipSuccess;
+    hipLaunchKernelGGL(gather_kernel, dim3((g.slot + 255u) / 256u, (uint32_t)g.nshards), dim3(256), 0, st, g);
     return hipGetLastError();
 }
 

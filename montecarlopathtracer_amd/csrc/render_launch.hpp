@@ -108,6 +108,22 @@ struct KernelParams {
     const uint32_t* seeds;
     // primary rays (CUTracer.cu:202-203, double): H / W, and 2^-k when W = 2^k (else 0)
     double h_over_w, inv_w_pow2;
+    // 1: the reduction writes the plain mean of this call's samples (a device's
+    // shard of a multi-device render; gather_kernel applies the running mean)
+    int32_t raw_mean;
+};
+
+// Multi-device gather (capi.cpp render_multi): shard r of `nshards` wrote the
+// plain means of its owned tiles, packed tile-major, to src[r * slot ...]
+// (peer-copied to the primary device); gather_kernel unpermutes them into the
+// row-major framebuffer with the running mean of reduce_kernel, bit for bit.
+struct GatherParams {
+    const float4* src;                   // [nshards][slot]
+    float4* fb;                          // row-major W x H
+    uint32_t slot;                       // packed pixels per shard slot (>= every shard's count)
+    int32_t width, height, tile, tiles_x, nshards;
+    uint32_t prev_count;
+    int32_t mode;
 };
 
 // Wavefront pipeline workspace (wavefront.hip).  One batch = samples
@@ -146,6 +162,7 @@ int total_lanes_for(uint32_t image_bytes, int cus);
 hipError_t launch_render(const KernelParams& kp, int cus, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1,
                          hipEvent_t ev2, float4* fb, int* variant_out);
 hipError_t launch_reduce(const KernelParams& kp, float4* fb, hipStream_t st);
+hipError_t launch_gather(const GatherParams& g, hipStream_t st);
 #ifdef MCPT_PHASE_TIMING
 void read_lane_use(unsigned long long out[6]);      // diagnostic build only: megakernel
 void read_lane_use_wf(unsigned long long out[6]);   // wavefront extend

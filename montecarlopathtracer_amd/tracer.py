@@ -322,6 +322,9 @@ class Tracer:
         self.last_stats: dict = {}
 
     def initialize(self, devices: Sequence[int] = (0,)) -> int:   # CUTracer.cu:220-223 (cudaSetDevice(0))
+        """devices[0] holds the scene; more entries replicate scenes created afterwards
+        on this thread and split each render into interleaved tiles across them,
+        gathered to devices[0] (mcpt_init, include/mcpt.h) -- the same image."""
         arr = (C.c_int32 * len(devices))(*devices)
         return check(lib().mcpt_init(arr, len(devices)))
 

@@ -1,8 +1,10 @@
 // Drop-in check: code written against the reference's PW::Tracer API (the call
 // sequence of CVMCTracer/main.cpp:16-18) compiled against include/mcpt_pw_tracer.hpp.
 // ObjModel here is a minimal stand-in with the reference's member names; the
-// data comes from the library's own reader.  Usage: pw_tracer_dropin scene.obj out.bin
+// data comes from the library's own reader.
+// Usage: pw_tracer_dropin scene.obj out.bin [devices, e.g. 0,0 -> Initialize({0, 0})]
 #include <cstdio>
+#include <cstdlib>
 #include <map>
 #include <string>
 #include <vector>
@@ -59,7 +61,14 @@ int main(int argc, char** argv) {
 
     const int W = 40, H = 30;
     std::vector<Vec3> hostcolor(W * H);
-    if (PW::Tracer::Initialize() != 0 || PW::Tracer::CreateGeometry(&model) != 0 ||
+    std::vector<int32_t> devices;
+    for (const char* c = argc > 3 ? argv[3] : ""; *c;) {
+        char* end = nullptr;
+        devices.push_back(static_cast<int32_t>(std::strtol(c, &end, 10)));
+        c = *end ? end + 1 : end;
+    }
+    const int init = devices.empty() ? PW::Tracer::Initialize() : PW::Tracer::Initialize(devices);
+    if (init != 0 || PW::Tracer::CreateGeometry(&model) != 0 ||
         PW::Tracer::RenderScene(1, hostcolor.data(), W, H, 3, 4) != 0) {
         std::printf("tracer: %s\n", mcpt_last_error());
         return 1;
