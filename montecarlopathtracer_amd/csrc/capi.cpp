@@ -897,7 +897,7 @@ int mcpt_model_group(const mcpt_model* m, int64_t g, char* name_buf, int64_t nam
     std::advance(it, g);
     if (name_buf && name_cap > 0) std::snprintf(name_buf, static_cast<size_t>(name_cap), "%s", it->first.c_str());
     if (n) *n = static_cast<int64_t>(it->second.size());
-    if (tris) std::memcpy(tris, it->second.data(), it->second.size() * sizeof(int32_t));
+    if (tris && !it->second.empty()) std::memcpy(tris, it->second.data(), it->second.size() * sizeof(int32_t));
     return MCPT_OK;
 }
 

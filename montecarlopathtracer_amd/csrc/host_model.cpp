@@ -10,6 +10,7 @@
 #include "host_model.hpp"
 
 #include <algorithm>
+#include <cmath>
 #include <cctype>
 #include <cfloat>
 #include <cstdio>
@@ -263,9 +264,15 @@ void build_host_scene(const ObjModel& m, HostScene& hs, const char* kd_cache_dir
     for (int64_t i = 0; i < ntri; ++i) {
         if (geom_of[static_cast<size_t>(i)] < 0) continue;
         const ObjTriangle& t = m.triangles[static_cast<size_t>(i)];
-        for (int j = 0; j < 3; ++j)
+        for (int j = 0; j < 3; ++j) {
             if (t.v[j] < 0 || t.v[j] >= nv || t.n[j] < 0 || t.n[j] >= nn)
                 throw Error{MCPT_E_INVALID, "triangle " + std::to_string(i) + " has an out-of-range index"};
+            // a non-finite vertex makes every KD box it touches inf/NaN (the
+            // reference renders garbage there); refuse it
+            const Vec3& p = m.vertices[static_cast<size_t>(t.v[j])];
+            if (!std::isfinite(p.x) || !std::isfinite(p.y) || !std::isfinite(p.z))
+                throw Error{MCPT_E_INVALID, "triangle " + std::to_string(i) + " has a non-finite vertex"};
+        }
         hs.kd_tris.push_back(static_cast<int32_t>(i));
         hs.kd_geom.push_back(static_cast<uint32_t>(geom_of[static_cast<size_t>(i)]));
         hs.kd_prio.push_back(rank_of[static_cast<size_t>(i)]);
@@ -362,6 +369,16 @@ void build_kdtree(const std::vector<float>& tv, std::vector<KdNode>& out,
     nodes[0].box = node_box(nodes[0].ids);
     std::deque<int32_t> work{0};
     int max_depth = 0;
+    // The reference duplicates straddling triangles into both children down to
+    // depth 32 (KDTree.hpp:103-153): triangles that straddle every split (long
+    // slivers, a polygon fan) make that exponential -- the reference would
+    // exhaust memory.  Budget: nodes and triangle references held by nodes
+    // under construction stay within generous multiples of the input (the
+    // bundled scenes and the 70k C4 mesh use <= 14 nodes and <= 15 references
+    // per triangle); a build past it is refused instead of taking the host down.
+    const uint64_t node_budget = std::max<uint64_t>(uint64_t(1) << 20, uint64_t(64) * n);
+    const uint64_t ref_budget = std::max<uint64_t>(uint64_t(1) << 24, uint64_t(256) * n);
+    uint64_t live_refs = n;
 
     struct Cand { float v; uint32_t ins; };
     std::vector<Cand> cands;
@@ -428,7 +445,13 @@ void build_kdtree(const std::vector<float>& tv, std::vector<KdNode>& out,
         nodes[ni].split = val;
         nodes[ni].left = static_cast<int32_t>(nodes.size());
         nodes[ni].right = static_cast<int32_t>(nodes.size() + 1);
+        live_refs += l.ids.size() + r.ids.size();
+        live_refs -= nodes[ni].ids.size();
         std::vector<uint32_t>().swap(nodes[ni].ids);
+        if (nodes.size() + 2 > node_budget || live_refs > ref_budget)
+            throw Error{MCPT_E_UNSUPPORTED, "KD build exceeds its budget (" + std::to_string(nodes.size() + 2) +
+                                                " nodes, " + std::to_string(live_refs) +
+                                                " triangle references): straddling triangles duplicate without bound"};
         nodes.push_back(std::move(l));
         nodes.push_back(std::move(r));
         work.push_back(static_cast<int32_t>(nodes.size() - 2));

@@ -136,6 +136,14 @@ bool kd_cache_load(const std::string& dir, const std::vector<float>& tv, std::ve
               h.key_a == ka && h.key_b == kb && h.n_nodes > 0 && h.n_nodes < (1ull << 31) &&
               h.n_leaf_ids < (1ull << 31) && h.depth >= 0 && h.depth <= kMaxKdDepth;
     if (ok) {
+        // the payload must be exactly what the header announces: checked against
+        // the file size before anything is allocated (a crafted header cannot make
+        // the reader reserve up to 2^31 x 48 B)
+        const uint64_t want = sizeof(Header) + h.n_nodes * kNodeWords * 4 + h.n_leaf_ids * 4;
+        ok = std::fseek(f, 0, SEEK_END) == 0 && std::ftell(f) >= 0 && uint64_t(std::ftell(f)) == want &&
+             std::fseek(f, long(sizeof(Header)), SEEK_SET) == 0;
+    }
+    if (ok) {
         w.resize(size_t(h.n_nodes) * kNodeWords);
         ids.resize(size_t(h.n_leaf_ids));
         ok = std::fread(w.data(), 4, w.size(), f) == w.size() && std::fread(ids.data(), 4, ids.size(), f) == ids.size();

@@ -300,3 +300,22 @@ def test_kd_cache_rejects_crafted_files_with_valid_hashes(mcpt, tmp_path):
     assert not loads()
     # the last state rebuilt and rewrote the file: it loads again
     assert loads()
+
+
+def test_runaway_kd_build_and_non_finite_vertices_are_refused(mcpt, tmp_path):
+    """Found by scripts/sanitize.sh's malformed corpus: a 1000-vertex polygon fan
+    (every sliver straddles every split) makes the reference's KD build
+    (KDTree.hpp:103-153, straddlers duplicated down to depth 32) duplicate
+    without bound -- 45 GB before it was stopped.  The build now refuses past
+    its node / reference budget; a non-finite vertex is refused too."""
+    ngon = tmp_path / "ngon.obj"
+    ngon.write_text("".join(f"v {i} {i % 7} {i % 3}\n" for i in range(1, 1001)) + "vn 0 0 1\nf " +
+                    " ".join(f"{i}//1" for i in range(1, 1001)) + "\n")
+    with pytest.raises(mcpt.McptError) as e:
+        mcpt.Scene(mcpt.ObjModel(str(ngon)), host_only=True)
+    assert e.value.code == -6 and "budget" in str(e.value)
+    bad = tmp_path / "inf.obj"
+    bad.write_text("v 0 0 0\nv 1e999 0 0\nv 0 1 0\nvn 0 0 1\nf 1//1 2//1 3//1\n")
+    with pytest.raises(mcpt.McptError) as e:
+        mcpt.Scene(mcpt.ObjModel(str(bad)), host_only=True)
+    assert e.value.code == -1 and "non-finite" in str(e.value)
