@@ -248,8 +248,9 @@ class Scene:
         self.host_only = host_only
 
     def close(self):
-        if self._h is not None and _capi._lib is not None:
-            _capi._lib.mcpt_scene_destroy(self._h)
+        h = getattr(self, "_h", None)   # None also when __init__ failed
+        if h is not None and _capi._lib is not None:
+            _capi._lib.mcpt_scene_destroy(h)
         self._h = None
 
     __del__ = close
