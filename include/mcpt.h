@@ -220,9 +220,9 @@ int64_t mcpt_shard_pixel_count(const mcpt_render_params* p);
 int mcpt_shard_pixels(const mcpt_render_params* p, int32_t* xy);      /* count*2 */
 /* reserve device workspace for p so mcpt_render_device allocates nothing
  * (required before hipGraph capture).  Megakernel workspace per render:
- * partial sums 16 B x pixels x ceil(spp/chunk), the RNG seed table 4 B per
- * path (pixels x spp, when below 2^31 paths; C2: 4 GiB), the stack spill area
- * (32 x 16 B per lane); wavefront: 160 B per path of the batch.             */
+ * partial sums 16 B x pixels x ceil(spp/chunk), the tail-split buffer (16 B
+ * per sample of the last ~4 units per lane) and the stack spill area (32 x
+ * 16 B per lane); wavefront: 160 B per path of the batch.                    */
 int mcpt_scene_reserve(mcpt_scene* s, const mcpt_render_params* p);
 
 #ifdef __cplusplus

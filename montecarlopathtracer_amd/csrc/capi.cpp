@@ -91,8 +91,6 @@ struct Workspace {
     size_t wf_bytes = 0;
     void* tail = nullptr;        // megakernel tail split: one float4 per tail sample
     size_t tail_bytes = 0;
-    void* seeds = nullptr;       // megakernel RNG seed table: one uint32 per (unit, sample)
-    size_t seeds_bytes = 0;
 };
 
 struct Timing {
@@ -132,7 +130,7 @@ struct mcpt_scene {
         (void)hipGetDevice(&prev);
         (void)hipSetDevice(device);
         (void)hipDeviceSynchronize();
-        for (void* p : {d_image, d_normals, ws.partial, ws.small, ws.spill, ws.fb, ws.wf, ws.tail, ws.seeds, gather})
+        for (void* p : {d_image, d_normals, ws.partial, ws.small, ws.spill, ws.fb, ws.wf, ws.tail, gather})
             if (p) (void)hipFree(p);
         for (auto& t : pending) for (auto ev : t.e) (void)hipEventDestroy(ev);
         for (auto& t : free_timing) for (auto ev : t.e) (void)hipEventDestroy(ev);
@@ -470,27 +468,6 @@ void prepare_workspace(mcpt_scene& s, mcpt::KernelParams& k, bool tail_split = f
     k.tail_units = k.total_units;
     k.total_items = k.total_units;
     k.tail_buf = nullptr;
-    k.seeds = nullptr;
-    // megakernel: RNG seed table, 4 B per path (C2: 4 GiB; entries < 2^31, i.e.
-    // <= 8 GiB, else the path kernel seeds in place); MCPT_SEED_TABLE=0 disables
-    const uint64_t seed_entries = uint64_t(k.total_units) * k.chunk;
-    const char* es = std::getenv("MCPT_SEED_TABLE");
-    if (tail_split && seed_entries > 0 && seed_entries < (uint64_t(1) << 31) && !(es && std::atoi(es) == 0)) {
-        // the table is an optimisation: without the memory for it, seed in place
-        const size_t need = size_t((seed_entries + 3) / 4) * 16;              // seed_kernel: 4 per store
-        if (s.ws.seeds_bytes < need || !s.ws.seeds) {
-            if (s.ws.seeds) HIP_TRY(hipFree(s.ws.seeds));
-            s.ws.seeds = nullptr;
-            s.ws.seeds_bytes = 0;
-            if (hipMalloc(&s.ws.seeds, need) == hipSuccess) {
-                s.ws.seeds_bytes = need;
-            } else {
-                s.ws.seeds = nullptr;
-                (void)hipGetLastError();                                    // clear the sticky error
-            }
-        }
-        if (s.ws.seeds) k.seeds = static_cast<const uint32_t*>(s.ws.seeds);
-    }
     if (tail_split && k.chunk > 1) {
         // MCPT_TAIL_UNITS: exact count (tests); MCPT_TAIL_UNITS_PER_LANE: per lane
         const char* e = std::getenv("MCPT_TAIL_UNITS_PER_LANE");

@@ -12,7 +12,7 @@
 //   Cramer test           CVMCTracer/CUDA/CUTracer.cu:54-92
 //   sampleHemi/Phong/Fresnel  CVMCTracer/CUDA/Utils.hpp:46-137
 //   normalize()           CVMCTracer/CUDA/Utils.hpp:27-34
-//   TEA-16 / Park-Miller  MCRT/QuinEngine/Shader/rtx.hlsl:61-82
+//   TEA-16 / Park-Miller  MCRT/QuinEngine/Shader/rtx.hlsl:61-82 (path seeds: PCG hash)
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -176,8 +176,20 @@ __device__ __forceinline__ uint32_t tea16(uint32_t v0, uint32_t v1) {   // rtx.h
     }
     return v0;
 }
+// PCG hash (Jarzynski & Olano, "Hash Functions for GPU Rendering", JCGT 9(3),
+// 2020: the PCG RXS-M-XS output permutation of one LCG step -- a bijection of
+// 32-bit words with good avalanche at ~6 integer ops, where TEA needs many of
+// its 16 rounds for the same quality)
+__device__ __forceinline__ uint32_t pcg_hash(uint32_t x) {
+    const uint32_t st = x * 747796405u + 2891336453u;
+    const uint32_t w = ((st >> ((st >> 28u) + 4u)) ^ st) * 277803737u;
+    return (w >> 22u) ^ w;
+}
+// Park-Miller start state of sample `sample` of pixel `pixel` (CVMCTracer mode;
+// DESIGN.md section 3): stateless per (pixel, sample), so every sharding,
+// chunking and kernel structure draws the same stream
 __device__ __forceinline__ uint32_t rng_init(uint32_t pixel, uint32_t key, uint32_t sample) {
-    return 1u + tea16(pixel, key + sample) % 0x7FFFFFFEu;
+    return 1u + pcg_hash(pcg_hash(pixel ^ key) + sample) % 0x7FFFFFFEu;
 }
 __device__ __forceinline__ float rng_next(uint32_t& sd) {   // rtx.hlsl:74-82
     uint32_t s = sd;

@@ -12,8 +12,8 @@
 //     LDS once per workgroup; the KD traversal stack keeps up to S entries in
 //     LDS (lane-strided, conflict-free, managed lazily) and older ones in
 //     global memory;
-//   * RNG seeds of every path from a full-wave pre-pass (seed_kernel), the
-//     next sample's seed prefetched while a path traces;
+//   * the RNG seed of every path from its (pixel, sample) by a PCG hash, at the
+//     path's start (stateless: any scheduling draws the same streams);
 //   * ordered front-to-back KD traversal (split-plane intervals, conservative
 //     2^-12 margins) returning the brute-force closest hit (ties broken in the
 //     brute-force loop order), see DESIGN.md;
@@ -92,7 +92,6 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
     int mode = kNeed;
     SlotCursor units = {0, kChunk};
     uint32_t s = 0, s_end = 0, unit_id = 0;
-    uint32_t seed_base = 0, seed_nx = 0;   // seed table: this unit's entries - s; next sample's seed
     int px = 0, py = 0, depth = 0;
     uint32_t sd = 1;
     V3 part = v3(0, 0, 0), color = v3(1, 1, 1);
@@ -101,17 +100,9 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
     r.d = v3(0, 0, -1);
     r.htri = -1;
 
-    // sample s of the current unit: its primary ray (the caller then starts it).
-    // With the seed table the sample's seed was prefetched when the previous
-    // sample of the unit started (first sample: read now), and the next one's
-    // load is issued here, in flight while this path traces.
-    auto new_path = [&](bool first) {
-        if (kp.seeds) {
-            sd = first ? kp.seeds[seed_base + s] : seed_nx;
-            if (s + 1u < s_end) seed_nx = kp.seeds[seed_base + s + 1u];
-        } else {
-            sd = path_seed(kp, (uint32_t)py * (uint32_t)kp.width + (uint32_t)px, s);
-        }
+    // sample s of the current unit: its primary ray (the caller then starts it)
+    auto new_path = [&]() {
+        sd = path_seed(kp, (uint32_t)py * (uint32_t)kp.width + (uint32_t)px, s);
         if constexpr (QE) {
             primary_ray_qe_sd(kp, px, py, sd, r.o, r.d);
         } else {
@@ -169,7 +160,6 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
                     const uint32_t v = u - chunk * kp.npix_local;
                     s = chunk * kp.chunk + j;
                     s_end = min(s + cnt, kp.spp);
-                    seed_base = u * kp.chunk - chunk * kp.chunk;   // entry u * chunk + j = seed_base + s
                     // partial index, or the tail sample's slot with the top bit set
                     unit_id = single ? (0x80000000u | (unit - kp.tail_units)) : u;
                     if constexpr (DBG) c0 = c;
@@ -177,7 +167,7 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
                     if (s >= s_end) {
                         // sample past spp in a ragged last chunk: nothing to do, take another item
                     } else if (unit_pixel(kp, v, px, py)) {
-                        new_path(true);
+                        new_path();
                         start_ray();
                     } else {
                         store_part(kp, unit_id, part);
@@ -273,7 +263,7 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
                     }
                     mode = kNeed;
                 } else {
-                    new_path(false);
+                    new_path();
                     cont = true;
                 }
             }
@@ -301,48 +291,6 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
     }
 #endif
     flush_counters(c, kp.stats);
-}
-
-// RNG seed table: every (unit, sample) path's seed, computed by full waves
-// here instead of inside the path kernel's shading rounds, where the 16-round
-// TEA ran for the few lanes whose path had just ended (6.5% of the frame).
-// Four entries per thread: four independent TEA chains interleave (one chain
-// alone waits on each dependent integer op), one 16-B store.  The table is
-// padded to a multiple of 4 entries.
-__global__ void __launch_bounds__(256) seed_kernel(const KernelParams kp, uint4* __restrict__ seeds) {
-    const uint32_t n = kp.total_units * kp.chunk, nq = (n + 3u) / 4u;
-    for (uint32_t q = blockIdx.x * 256u + threadIdx.x; q < nq; q += gridDim.x * 256u) {
-        uint32_t pix[4], smp[4];
-        bool ok[4];
-        if ((kp.chunk & 3u) == 0u) {          // the quad lies in one unit: decode it once
-            const uint32_t i = 4u * q;
-            const uint32_t u = kp.div_chunk.div(i), j = i - u * kp.chunk;
-            const uint32_t ch = kp.div_npix.div(u), v = u - ch * kp.npix_local;
-            int x = 0, y = 0;
-            const bool in = i < n && unit_pixel(kp, v, x, y);
-#pragma unroll
-            for (int e = 0; e < 4; e++) {
-                smp[e] = ch * kp.chunk + j + (uint32_t)e;
-                ok[e] = in && smp[e] < kp.spp;
-                pix[e] = (uint32_t)y * (uint32_t)kp.width + (uint32_t)x;
-            }
-        } else {
-#pragma unroll
-            for (int e = 0; e < 4; e++) {
-                const uint32_t i = 4u * q + (uint32_t)e;
-                const uint32_t u = kp.div_chunk.div(i), j = i - u * kp.chunk;
-                const uint32_t ch = kp.div_npix.div(u), v = u - ch * kp.npix_local;
-                smp[e] = ch * kp.chunk + j;
-                int x = 0, y = 0;
-                ok[e] = i < n && smp[e] < kp.spp && unit_pixel(kp, v, x, y);
-                pix[e] = (uint32_t)y * (uint32_t)kp.width + (uint32_t)x;
-            }
-        }
-        uint32_t sd[4];
-#pragma unroll
-        for (int e = 0; e < 4; e++) sd[e] = path_seed(kp, pix[e], smp[e]);
-        seeds[q] = make_uint4(ok[0] ? sd[0] : 0u, ok[1] ? sd[1] : 0u, ok[2] ? sd[2] : 0u, ok[3] ? sd[3] : 0u);
-    }
 }
 
 // running mean of a pixel (CUTracer.cu:214-217; QE gamma-space, rtx.hlsl:401-402):
@@ -435,12 +383,6 @@ hipError_t launch_render(const KernelParams& kp_in, int cus, hipStream_t st, hip
     kp.total_lanes = (uint32_t)total_lanes_for(img, cus);
     hipError_t e = hipMemsetAsync(kp.counter, 0, sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
-    if (kp.seeds) {   // before ev0: the events time the path kernel alone (rocprof's figure)
-        const uint32_t nq = (kp.total_units * kp.chunk + 3u) / 4u, blocks = (nq + 255u) / 256u;
-        hipLaunchKernelGGL(seed_kernel, dim3(blocks < 64u * (uint32_t)cus ? blocks : 64u * (uint32_t)cus), dim3(256),
-                           0, st, kp, reinterpret_cast<uint4*>(const_cast<uint32_t*>(kp.seeds)));
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-    }
     if (ev0) hipEventRecord(ev0, st);
     int variant = 0;
     if (kp.scene.node_boxes) {                     // image built for global memory

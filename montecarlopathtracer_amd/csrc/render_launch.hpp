@@ -102,10 +102,6 @@ struct KernelParams {
     uint32_t tail_units, total_items;
     FastDiv div_chunk;                   // chunk
     float4* tail_buf;
-    // RNG seed table (megakernel): seeds[u * chunk + j] = path_seed of sample j
-    // of unit u, written by seed_kernel before the path kernel (nullptr: the
-    // path kernel computes TEA-16 itself)
-    const uint32_t* seeds;
     // primary rays (CUTracer.cu:202-203, double): H / W, and 2^-k when W = 2^k (else 0)
     double h_over_w, inv_w_pow2;
     // 1: the reduction writes the plain mean of this call's samples (a device's

@@ -106,6 +106,7 @@ void orc_copy_kd_leaf_ids(const orc_scene* s, uint32_t* out);
 /* building blocks for known-answer tests ---------------------------------- */
 float orc_det3(const float* m9);                                 /* Math.hpp:169-175 */
 uint32_t orc_tea16(uint32_t v0, uint32_t v1);
+uint32_t orc_pcg_hash(uint32_t x);
 uint32_t orc_rng_init(uint32_t pixel, uint32_t key, uint32_t sample);
 float orc_rng_next(uint32_t* state);
 uint32_t orc_seed_key(uint64_t seed);

@@ -76,6 +76,8 @@ def lib():
         L.orc_det3.argtypes = [f32p]
         L.orc_tea16.restype = C.c_uint32
         L.orc_tea16.argtypes = [C.c_uint32, C.c_uint32]
+        L.orc_pcg_hash.restype = C.c_uint32
+        L.orc_pcg_hash.argtypes = [C.c_uint32]
         L.orc_rng_init.restype = C.c_uint32
         L.orc_rng_init.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32]
         L.orc_rng_next.restype = C.c_float

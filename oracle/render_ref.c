@@ -122,8 +122,17 @@ uint32_t orc_tea16(uint32_t v0, uint32_t v1) {
     return v0;
 }
 uint32_t orc_seed_key(uint64_t seed) { return orc_tea16((uint32_t)seed, (uint32_t)(seed >> 32)); }
+/* Path seed of CVMCTracer mode (our determinism spec; the
+ * reference seeds irreproducible cuRAND streams, CUTracer.cu:186-187): PCG hash
+ * of (pixel ^ key) then of that + sample (Jarzynski & Olano, "Hash Functions for
+ * GPU Rendering", JCGT 9(3) 2020), onto the Park-Miller range [1, 2^31 - 2] */
+uint32_t orc_pcg_hash(uint32_t x) {
+    uint32_t st = x * 747796405u + 2891336453u;
+    uint32_t w = ((st >> ((st >> 28u) + 4u)) ^ st) * 277803737u;
+    return (w >> 22u) ^ w;
+}
 uint32_t orc_rng_init(uint32_t pixel, uint32_t key, uint32_t sample) {
-    return 1u + orc_tea16(pixel, key + sample) % 0x7FFFFFFEu;
+    return 1u + orc_pcg_hash(orc_pcg_hash(pixel ^ key) + sample) % 0x7FFFFFFEu;
 }
 /* QE/Shader/rtx.hlsl:74-82 (Park-Miller via Schrage); u = float(sd) / 2^31 */
 float orc_rng_next(uint32_t* sd) {

@@ -6,7 +6,7 @@
 set -e
 O=gpurun_out/lines
 mkdir -p $O
-B="python bench.py --no-cpu-baseline"
+B="python bench.py --no-cpu-baseline --no-pmc"
 timeout -k 10 300 $B --pipeline wavefront --steps 3 --warmup 1 > $O/c2_wavefront.jsonl 2> $O/c2_wavefront.err
 timeout -k 10 300 $B --scene cornell_bunny70k --spp 256 --steps 2 --warmup 1 > $O/c4_megakernel.jsonl 2> $O/c4_megakernel.err
 timeout -k 10 300 $B --scene cornell_bunny70k --spp 256 --pipeline wavefront --steps 2 --warmup 1 > $O/c4_wavefront.jsonl 2> $O/c4_wavefront.err

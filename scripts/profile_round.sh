@@ -11,7 +11,7 @@ OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 cd /tmp
-B="python3 $R/bench.py --no-cpu-baseline $BENCH_ARGS"
+B="python3 $R/bench.py --no-cpu-baseline --no-pmc $BENCH_ARGS"
 timeout -k 10 300 $B --steps 3 --warmup 1 > $OUT/bench.jsonl 2> $OUT/bench.err
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o run -- $B --steps 2 --warmup 1 > $OUT/kt.log 2>&1
 pass() {   # name counters...

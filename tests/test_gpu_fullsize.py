@@ -5,8 +5,8 @@ statistical pin against the reference's own 1000-spp render.
   tile shards (configs[2]'s partition) and reassembling them reproduces the
   single-GPU image bit for bit; a second render is bit-identical (determinism);
   the image is finite and the light is the brightest region.
-* the same frame through the wavefront pipeline and through the megakernel
-  without its seed table: bit-identical images, equal counters.
+* the same frame through the wavefront pipeline: bit-identical image, equal
+  counters.
 * RenderScene's progressive loop (10 launches x 100 spp, prevCount running
   mean, CUTracer.cu:378-398) at 800x600 with the published-render variant
   (luminance 30, untinted Fresnel) matches CV/result1.png statistically.
@@ -56,29 +56,25 @@ def test_fullsize_shards_and_determinism(mcpt, scene01):
     assert torch.equal(got[:, :3], full[:, :3])
 
 
-def test_fullsize_pipelines_agree(mcpt, scene01, monkeypatch):
+def test_fullsize_pipelines_agree(mcpt, scene01):
     """C2 at full size through two independent implementations: the wavefront
-    pipeline (per-bounce queues) and the megakernel with in-kernel seeding
-    (MCPT_SEED_TABLE=0) render the default megakernel's image bit for bit, with
-    equal work counters."""
+    pipeline (per-bounce queues) renders the megakernel's image bit for bit,
+    with equal work counters."""
     import torch
     W = H = 1024
     stream = torch.cuda.current_stream().cuda_stream
     out = {}
-    for name, pipeline, table in (("mega", "megakernel", "1"), ("wave", "wavefront", "1"),
-                                  ("mega_noseed", "megakernel", "0")):
-        monkeypatch.setenv("MCPT_SEED_TABLE", table)
+    for name, pipeline in (("mega", "megakernel"), ("wave", "wavefront")):
         p = mcpt.RenderParams(width=W, height=H, spp=1024, spp_chunk=32, pipeline=pipeline)
         fb = torch.zeros((H * W, 4), dtype=torch.float32, device="cuda")
         scene01.render_device(p, fb.data_ptr(), stream)
         torch.cuda.synchronize()
         out[name] = (fb, scene01.stats())
     ref, rs = out["mega"]
-    for name in ("wave", "mega_noseed"):
-        img, st = out[name]
-        assert torch.equal(img[:, :3], ref[:, :3]), name
-        for k in ("rays", "paths", "inner_visits", "leaf_visits", "tri_tests", "shades"):
-            assert st[k] == rs[k], (name, k, st[k], rs[k])
+    img, st = out["wave"]
+    assert torch.equal(img[:, :3], ref[:, :3])
+    for k in ("rays", "paths", "inner_visits", "leaf_visits", "tri_tests", "shades"):
+        assert st[k] == rs[k], (k, st[k], rs[k])
 
 
 def test_progressive_render_matches_reference_image(mcpt):

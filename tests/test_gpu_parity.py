@@ -240,10 +240,10 @@ def test_tail_split_is_bit_identical(mcpt, oracle_mod, monkeypatch, tail):
 
 
 @pytest.mark.parametrize("mode", ["cv", "qe"])
-def test_seed_table_matches_in_kernel_seeding(mcpt, oracle_mod, monkeypatch, mode):
-    """The megakernel's RNG seed table (seed_kernel, next seed prefetched) and the
-    in-kernel TEA-16 fallback (MCPT_SEED_TABLE=0) render the oracle's image bit for
-    bit, with ragged chunks and the tail split active."""
+def test_ragged_chunks_with_tail_split_match_oracle(mcpt, oracle_mod, mode):
+    """Path seeds computed in the kernel at each path's start (PCG hash in CV
+    mode, TEA-16 in QE mode) with ragged chunks and the tail split active: the
+    oracle's image bit for bit and its counters."""
     path = mcpt.scene_path("scene01")
     W, H, spp, chunk = 36, 28, 9, 4
     if mode == "qe":
@@ -255,12 +255,10 @@ def test_seed_table_matches_in_kernel_seeding(mcpt, oracle_mod, monkeypatch, mod
         ref, rc = _oracle_render(oracle_mod, path, W, H, spp, chunk, 7, 31, 1, 10.0, 1, node_boxes=_node_boxes(mcpt, path))
         p = mcpt.RenderParams.for_scene(1, width=W, height=H, spp=spp, spp_chunk=chunk, seed=31)
     scene = mcpt.Scene(mcpt.ObjModel(path))
-    for table in ("1", "0"):
-        monkeypatch.setenv("MCPT_SEED_TABLE", table)
-        img, st = scene.render(p)
-        assert np.array_equal(img, ref), (table, float(np.abs(img - ref).max()))
-        for k in ("rays", "paths", "inner_visits", "leaf_visits", "leaf_refs", "tri_tests", "shades"):
-            assert st[k] == rc[k], (table, k, st[k], rc[k])
+    img, st = scene.render(p)
+    assert np.array_equal(img, ref), float(np.abs(img - ref).max())
+    for k in ("rays", "paths", "inner_visits", "leaf_visits", "leaf_refs", "tri_tests", "shades"):
+        assert st[k] == rc[k], (k, st[k], rc[k])
 
 
 @pytest.mark.parametrize("sc", ["scene01", "cornell_bunny70k"])

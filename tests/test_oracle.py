@@ -219,6 +219,25 @@ def test_rng_is_minimal_standard_park_miller(oracle_mod):
     assert len(keys) == 64 * 64 and min(keys) >= 1 and max(keys) <= 0x7FFFFFFE
 
 
+def test_pcg_path_seeds_known_answer(oracle_mod):
+    """CV-mode path seeds: PCG hash (Jarzynski & Olano 2020)
+    restated here in numpy, composed as 1 + pcg(pcg(pixel ^ key) + sample) mod
+    (2^31 - 2), equal to the oracle's (and, in tests/test_gpu_math.py, the device's)."""
+    def pcg(x):
+        x = np.asarray(x, np.uint64) & 0xFFFFFFFF
+        st = (x * 747796405 + 2891336453) & 0xFFFFFFFF
+        w = (((st >> ((st >> 28) + 4)) ^ st) * 277803737) & 0xFFFFFFFF
+        return (w >> 22) ^ w
+    L = oracle_mod.lib()
+    r = np.random.default_rng(9)
+    xs = r.integers(0, 2**32, 500, dtype=np.uint64)
+    assert [int(v) for v in pcg(xs)] == [L.orc_pcg_hash(int(v)) for v in xs]
+    assert int(pcg(0)) == L.orc_pcg_hash(0)
+    for pix, key, smp in [(0, 0, 0), (5, 123, 7), (2**20, 0xDEADBEEF, 1023), (2**32 - 1, 2**32 - 1, 2**32 - 1)]:
+        want = 1 + int(pcg((int(pcg(pix ^ key)) + smp) & 0xFFFFFFFF)) % 0x7FFFFFFE
+        assert L.orc_rng_init(pix, key, smp) == want
+
+
 def test_statistical_pin_against_reference_render(scenes, oracle_mod):
     """CV/result1.png (1000 spp, 8-bit) was rendered with luminance 30 (MC.docx ¶58)
     and without the Kd tint on Fresnel hits (the rtx.hlsl:345 form).  100x100
