@@ -54,7 +54,9 @@ constexpr int kNeed = 3;    // needs a work unit
 struct RayState {
     V3 o, d;
     float ix, iy, iz;
-    float tmin, tmax, best;
+    float tmin;
+    float tmax;                          // the interval's far end times kEpsHi (rounded), see begin_ray
+    float best;
     uint32_t nw0, nw1, bprio;            // current node record
     int32_t sp, htri;
     int32_t lo;                          // stack entries [0, lo) live in the spill memory
@@ -93,51 +95,95 @@ __device__ __forceinline__ bool begin_ray(RayState& r, const GpuScene& sc, float
         }
     }
     r.tmin = tmin;
-    r.tmax = tmax;
-    return !miss && !(tmin > tmax * kEpsHi);
+    // the walk compares against tmax only as tmax * kEpsHi, so the state keeps
+    // that product: RN(x * kEpsHi) is monotone in x, hence RN(min(t, tmax) * kEpsHi)
+    // = min(RN(t * kEpsHi), RN(tmax * kEpsHi)) and the interval updates keep it
+    // exactly (one multiply per descent step less; stack entries carry it too)
+    r.tmax = tmax * kEpsHi;
+    return !miss && !(tmin > r.tmax);
 }
 
 // Cramer test (CUTracer.cu:54-92) with an exact-result-preserving prefilter:
 // the three IEEE divisions run only when the signs of the determinants allow
 // beta, gamma, t > 0 and the magnitudes do not already rule out beta+gamma < 1
 // or t < best (2^-20 margins cover every rounding of the exact path).
-__device__ __forceinline__ void test_tri_v(RayState& r, const float4 A0, const float4 A1, const float4 A2, uint32_t k) {
+struct TriDets {
+    float detA, qb, qg, qt;
+};
+__device__ __forceinline__ bool tri_prefilter(const RayState& r, const float4 A0, const float4 A1, const float4 A2,
+                                              TriDets& q) {
     const float aox = A0.x - r.o.x, aoy = A0.y - r.o.y, aoz = A0.z - r.o.z;
     // A2.w = A1.y * A2.z - A2.y * A1.z, precomputed (the last minor of det A and det tM)
-    const float detA = det3_m(A1.x, A2.x, r.d.x, A1.y, A2.y, r.d.y, A1.z, A2.z, r.d.z, A2.w);
-    const float qb = det3(aox, A2.x, r.d.x, aoy, A2.y, r.d.y, aoz, A2.z, r.d.z);
-    const float qg = det3(A1.x, aox, r.d.x, A1.y, aoy, r.d.y, A1.z, aoz, r.d.z);
-    const float qt = det3_m(A1.x, A2.x, aox, A1.y, A2.y, aoy, A1.z, A2.z, aoz, A2.w);
+    q.detA = det3_m(A1.x, A2.x, r.d.x, A1.y, A2.y, r.d.y, A1.z, A2.z, r.d.z, A2.w);
+    q.qb = det3(aox, A2.x, r.d.x, aoy, A2.y, r.d.y, aoz, A2.z, r.d.z);
+    q.qg = det3(A1.x, aox, r.d.x, A1.y, aoy, r.d.y, A1.z, aoz, r.d.z);
+    q.qt = det3_m(A1.x, A2.x, aox, A1.y, A2.y, aoy, A1.z, A2.z, aoz, A2.w);
     // sign-normalised numerators: beta, gamma, t > 0 needs all three > 0 (a NaN
     // anywhere means no hit, so min3 may drop it); detA == 0 fails the magnitude test
-    const uint32_t sA = __float_as_uint(detA) & 0x80000000u;
-    const float xb = __uint_as_float(__float_as_uint(qb) ^ sA);
-    const float xg = __uint_as_float(__float_as_uint(qg) ^ sA);
-    const float xt = __uint_as_float(__float_as_uint(qt) ^ sA);
+    const uint32_t sA = __float_as_uint(q.detA) & 0x80000000u;
+    const float xb = __uint_as_float(__float_as_uint(q.qb) ^ sA);
+    const float xg = __uint_as_float(__float_as_uint(q.qg) ^ sA);
+    const float xt = __uint_as_float(__float_as_uint(q.qt) ^ sA);
     const bool signs_ok = __builtin_fminf(__builtin_fminf(xb, xg), xt) > 0.0f;
-    const float adet = fabsf(detA) * 1.00000095367431640625f;   // 1 + 2^-20
+    const float adet = fabsf(q.detA) * 1.00000095367431640625f;   // 1 + 2^-20
     const bool mags_ok = !(xb + xg > adet) & !(xt > r.best * adet);
-    if (signs_ok & mags_ok) {
+    return signs_ok & mags_ok;
+}
+// the exact tail (IEEE quotients, CUTracer.cu:84-92) of a triangle whose prefilter passed
+__device__ __forceinline__ void tri_accept(RayState& r, const TriDets& q, uint32_t prio, uint32_t k) {
 #if MCPT_SHARED_DIV
-        const double rA = recip_shared(detA);
-        const float beta = div_shared(qb, rA);
-        const float gamma = div_shared(qg, rA);
-        const float t = div_shared(qt, rA);
+    const double rA = recip_shared(q.detA);
+    const float beta = div_shared(q.qb, rA);
+    const float gamma = div_shared(q.qg, rA);
+    const float t = div_shared(q.qt, rA);
 #else
-        const float beta = qb / detA;
-        const float gamma = qg / detA;
-        const float t = qt / detA;
+    const float beta = q.qb / q.detA;
+    const float gamma = q.qg / q.detA;
+    const float t = q.qt / q.detA;
 #endif
-        const uint32_t prio = __float_as_uint(A0.w);
-        if (beta + gamma < 1.0f && beta > 0.0f && gamma > 0.0f && t > 0.0f &&
-            (t < r.best || (t == r.best && prio < r.bprio))) {
-            r.best = t;
-            r.bprio = prio;
-            r.htri = (int32_t)k;
-            r.hbeta = beta;
-            r.hgamma = gamma;
-        }
+    if (beta + gamma < 1.0f && beta > 0.0f && gamma > 0.0f && t > 0.0f &&
+        (t < r.best || (t == r.best && prio < r.bprio))) {
+        r.best = t;
+        r.bprio = prio;
+        r.htri = (int32_t)k;
+        r.hbeta = beta;
+        r.hgamma = gamma;
     }
+}
+__device__ __forceinline__ void test_tri_v(RayState& r, const float4 A0, const float4 A1, const float4 A2, uint32_t k) {
+    TriDets q;
+    if (tri_prefilter(r, A0, A1, A2, q)) tri_accept(r, q, __float_as_uint(A0.w), k);
+}
+// Two triangles a, b of a leaf (b only if `two`): both prefilters first (b's
+// with the best before a's tail -- a larger best only widens the prefilter, the
+// exact tail still decides), then ONE exact tail for a lane's first candidate
+// (a, else b) and a second one only for lanes where both passed: a wave with
+// some lanes passing on a and others on b runs the tail once, not twice.  The
+// closest hit is the lexicographic minimum of (t, rank), so the tail order is
+// immaterial.
+#ifndef MCPT_TAIL_MERGE
+#define MCPT_TAIL_MERGE 1
+#endif
+__device__ __forceinline__ void test_tri_pair(RayState& r, const float4 A0, const float4 A1, const float4 A2,
+                                              uint32_t ka, const float4 B0, const float4 B1, const float4 B2,
+                                              uint32_t kb, bool two) {
+    TriDets qa, qb;
+    const bool oka = tri_prefilter(r, A0, A1, A2, qa);
+    const bool okb = tri_prefilter(r, B0, B1, B2, qb) & two;
+#if MCPT_TAIL_MERGE
+    if (oka | okb) {
+        TriDets q;
+        q.detA = oka ? qa.detA : qb.detA;
+        q.qb = oka ? qa.qb : qb.qb;
+        q.qg = oka ? qa.qg : qb.qg;
+        q.qt = oka ? qa.qt : qb.qt;
+        tri_accept(r, q, oka ? __float_as_uint(A0.w) : __float_as_uint(B0.w), oka ? ka : kb);
+    }
+    if (oka & okb) tri_accept(r, qb, __float_as_uint(B0.w), kb);
+#else
+    if (oka) tri_accept(r, qa, __float_as_uint(A0.w), ka);
+    if (okb) tri_accept(r, qb, __float_as_uint(B0.w), kb);
+#endif
 }
 __device__ __forceinline__ void test_tri(RayState& r, const float4* __restrict__ tris, uint32_t k) {
     test_tri_v(r, tris[3 * k], tris[3 * k + 1], tris[3 * k + 2], k);
@@ -277,8 +323,9 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
             const bool below = (oa < sv) | ((oa == sv) & (da <= 0.0f));
             // if/else chain of the oracle, evaluated branch-free
             const bool pp = (da == 0.0f) & (oa == sv);                  // ray inside the plane: both
-            const bool no = !(t > 0.0f) | (t > r.tmax * kEpsHi);        // near child only
-            const bool fo = t * kEpsHi < r.tmin;                        // far child only
+            const float te = t * kEpsHi;
+            const bool no = !(t > 0.0f) | (t > r.tmax);                 // near child only
+            const bool fo = te < r.tmin;                                // far child only
             const bool go_far = !pp & !no & fo;
             const bool both = !pp & !no & !fo;                          // push far, go near
             bool push_it = pp | both;
@@ -290,7 +337,6 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
                 far_ok = below ? hr : hl;
                 push_it = push_it & far_ok;
             }
-            const uint32_t n0 = below ? pr.x : pr.z, n1 = below ? pr.y : pr.w;     // near child record
             const uint32_t f0 = below ? pr.z : pr.x, f1 = below ? pr.w : pr.y;     // far child record
             if (push_it) {
                 const float plo = pp ? r.tmin : (t > r.tmin ? t : r.tmin);
@@ -308,12 +354,15 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
                 *slot = make_uint4(f0, f1, __float_as_uint(plo), __float_as_uint(r.tmax));
                 r.sp++;
                 if constexpr (!BOXES)                                   // here push_it & !pp == both
-                    if (!pp) r.tmax = t < r.tmax ? t : r.tmax;
+                    if (!pp) r.tmax = te < r.tmax ? te : r.tmax;
             }
             if constexpr (BOXES)                                        // the near child's interval,
-                if (both) r.tmax = t < r.tmax ? t : r.tmax;             // pushed far or not
-            w0 = go_far ? f0 : n0;
-            w1 = go_far ? f1 : n1;
+                if (both) r.tmax = te < r.tmax ? te : r.tmax;           // pushed far or not
+            // the child entered: the near one, or the far one when go_far (the
+            // left record when below != go_far) -- two selects, not four
+            const bool enter_left = below != go_far;
+            w0 = enter_left ? pr.x : pr.z;
+            w1 = enter_left ? pr.y : pr.w;
             if constexpr (BOXES) {
                 if (!(go_far ? far_ok : near_ok)) {   // the chosen child's box is missed: next interval
                     if (!pop_entry<S, !BOXES>(r, st, stride, spill, spill_stride)) return true;
@@ -343,14 +392,9 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
         const float4 a0 = tris[3 * k0], a1 = tris[3 * k0 + 1], a2 = tris[3 * k0 + 2];
         const float4 b0 = tris[3 * k1], b1 = tris[3 * k1 + 1], b2 = tris[3 * k1 + 2];
         MCPT_LANE_USE(tri_w, tri_l, lu);
-        if constexpr (COUNT) c.refs++;
-        if constexpr (COUNT) c.tests++;
-        test_tri_v(r, a0, a1, a2, k0);
-        if (two) {
-            if constexpr (COUNT) c.refs++;
-            if constexpr (COUNT) c.tests++;
-            test_tri_v(r, b0, b1, b2, k1);
-        }
+        if constexpr (COUNT) c.refs += two ? 2u : 1u;
+        if constexpr (COUNT) c.tests += two ? 2u : 1u;
+        test_tri_pair(r, a0, a1, a2, k0, b0, b1, b2, k1, two);
         r.lpos += two ? 2u : 1u;
     }
 #else
