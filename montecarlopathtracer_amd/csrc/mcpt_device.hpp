@@ -245,6 +245,41 @@ __device__ __forceinline__ V3 sample_phong(uint32_t& sd, V3 n, V3 in, float ns1)
     }
     return vsub(in, vscale(vscale(h, dot3(in, h)), 2.0f));
 }
+// Diffuse (sample_hemi) and Phong (sample_phong) in one body for a wave that
+// holds lanes of both materials: each lane draws its two uniforms and forms
+// (cos, sin) of its own lobe, then the sincos, the lobe vector and the frame
+// rotation -- the bulk of both samplers -- run once for all of them.  Per lane
+// the operations are exactly its sampler's: the rotation's y term is
+// d.z / invlen for Phong and d.z * (1 / invlen) for the hemisphere.
+// Returns the rotated lobe vector (the hemisphere direction, or Phong's half
+// vector before the reflection).
+__device__ __forceinline__ V3 sample_lobe(uint32_t& sd, V3 n, bool phong, float ns1) {
+    float x = rng_next(sd);
+    float y = rng_next(sd);
+    float cosT, sinT;
+    if (phong) {
+        cosT = pow_f(x, 1.0f / ns1);
+        sinT = sqrt_rn(1 - cosT * cosT);
+    } else {
+        sinT = sqrt_rn(x);
+        cosT = sqrt_rn(1 - x);
+    }
+    float phi = 2 * kPwPi * y;
+    float sp, cp;
+    sincos_f(phi, sp, cp);
+    V3 h = v3(sinT * cp, cosT, sinT * sp);
+    if (fabsf(n.y + 1) < kFltEps) {
+        h = v3(-h.x, -h.y, -h.z);
+    } else if (fabsf(n.y - 1) >= kFltEps) {
+        V3 d = h;
+        float invlen = 1.0f / sqrt_rn(1.0f - n.y * n.y);
+        const float q = (phong ? d.z : 1.0f) / invlen;
+        h.x = (n.z * d.x + n.x * n.y * d.z) * invlen + n.x * d.y;
+        h.y = n.y * d.y - (phong ? q : d.z * q);
+        h.z = (-n.x * d.x + n.z * n.y * d.z) * invlen + n.z * d.y;
+    }
+    return h;
+}
 // Fresnel: CVMCTracer normalizes only the refracted directions (epsilon-guarded
 // Utils.hpp:27-34; Utils.hpp:97-137); QuinEngine normalizes every output, the
 // mirror and total-internal-reflection branches included (rtx.hlsl:213-251)

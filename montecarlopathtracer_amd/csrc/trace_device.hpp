@@ -464,6 +464,9 @@ __device__ __forceinline__ V3 emitted(V3 color, const GpuGeom& g, float illum) {
 // n1..n3 are the hit triangle's vertex normals (fetched by the caller).  QE:
 // rtx.hlsl:336-358 -- HLSL normalize of the normal, QE Fresnel (always
 // normalized), Phong with the float Ns; fresnel_kd is 0 for QE (rtx.hlsl:345).
+#ifndef MCPT_MERGED_LOBE
+#define MCPT_MERGED_LOBE 1
+#endif
 template <bool QE = false>
 __device__ __forceinline__ void scatter_n(const GpuGeom& g, float4 n1, float4 n2, float4 n3, float hbeta,
                                           float hgamma, float best, int32_t fresnel_kd, uint32_t& sd, V3& color,
@@ -476,15 +479,31 @@ __device__ __forceinline__ void scatter_n(const GpuGeom& g, float4 n1, float4 n2
     if (g.Tr > 0) {
         dir = sample_fresnel<QE>(sd, nrm, dir, g.Tr, g.Ni);
         if (fresnel_kd) color = v3(color.x * g.Kd[0], color.y * g.Kd[1], color.z * g.Kd[2]);
-    } else if (g.Ns > 1) {
-        dir = sample_phong(sd, nrm, dir, QE ? g.Ns + 1.0f : (float)(g.Ns_u + 1u));
-        color = v3(color.x * g.Ks[0], color.y * g.Ks[1], color.z * g.Ks[2]);
     } else {
-        color = v3(color.x * g.Kd[0], color.y * g.Kd[1], color.z * g.Kd[2]);
-        // one inlined sampler for both sides (the flip only negates its result)
+#if MCPT_MERGED_LOBE
+        // Phong (Utils.hpp:72-95) and diffuse (:46-70) share one sampler body
+        const bool ph = g.Ns > 1;
         const bool flip = dot3(dir, nrm) > 0;
-        const V3 hd = sample_hemi(sd, nrm);
-        dir = flip ? v3(-hd.x, -hd.y, -hd.z) : hd;
+        const V3 h = sample_lobe(sd, nrm, ph, QE ? g.Ns + 1.0f : (float)(g.Ns_u + 1u));
+        if (ph) {
+            dir = vsub(dir, vscale(vscale(h, dot3(dir, h)), 2.0f));
+            color = v3(color.x * g.Ks[0], color.y * g.Ks[1], color.z * g.Ks[2]);
+        } else {
+            color = v3(color.x * g.Kd[0], color.y * g.Kd[1], color.z * g.Kd[2]);
+            dir = flip ? v3(-h.x, -h.y, -h.z) : h;
+        }
+#else
+        if (g.Ns > 1) {
+            dir = sample_phong(sd, nrm, dir, QE ? g.Ns + 1.0f : (float)(g.Ns_u + 1u));
+            color = v3(color.x * g.Ks[0], color.y * g.Ks[1], color.z * g.Ks[2]);
+        } else {
+            color = v3(color.x * g.Kd[0], color.y * g.Kd[1], color.z * g.Kd[2]);
+            // one inlined sampler for both sides (the flip only negates its result)
+            const bool flip = dot3(dir, nrm) > 0;
+            const V3 hd = sample_hemi(sd, nrm);
+            dir = flip ? v3(-hd.x, -hd.y, -hd.z) : hd;
+        }
+#endif
     }
     // hitPoint = pos + t*dir at the accepted t (CUTracer.cu:89-91), then
     // pos = hitPoint + dir*0.01 (:134,143,159)
