@@ -203,23 +203,19 @@ __device__ __forceinline__ void test_tri(RayState& r, const float4* __restrict__
 #define MCPT_LU_PARAM
 #define MCPT_LU_ARG
 #endif
-// Descent steps per call are capped at kDescentCap: a lane that has not
+// Descent steps per call are capped (MCPT_DESCENT_CAP): a lane that has not
 // reached a leaf keeps its node record and interval in RayState and resumes on
 // the next call, so the wave's descent loop is not as long as its deepest
-// lane's (lane use of the uncapped loop: 22%).  Likewise at most kTriCap
-// triangle tests per call, the leaf's remaining refs [lpos, lend) kept in
-// RayState (uncapped leaf loop: 35%).  Same visit order and counts.
+// lane's (lane use of the uncapped loop: 22%; cap sweep at the current kernel:
+// 3 / 4 / 5 / 6 -> 10.60 / 10.71 / 10.61 / 10.37 G rays/s).  Likewise two
+// triangle tests per call (a pair), the leaf's remaining refs [lpos, lend)
+// kept in RayState (uncapped leaf loop: 35%).  Same visit order and counts.
 #ifndef MCPT_DESCENT_CAP
-#define MCPT_DESCENT_CAP 5
+#define MCPT_DESCENT_CAP 4
 #endif
-#ifndef MCPT_TRI_CAP
-#define MCPT_TRI_CAP 2
+#ifndef MCPT_DESCENT_CAP_GLOBAL
+#define MCPT_DESCENT_CAP_GLOBAL 5                // global-memory scenes (C4: 5 > 4)
 #endif
-#ifndef MCPT_TRI_PAIR
-#define MCPT_TRI_PAIR 1
-#endif
-constexpr int kDescentCap = MCPT_DESCENT_CAP;
-constexpr uint32_t kTriCap = MCPT_TRI_CAP;
 // Child-box cull (scenes in global memory): each sibling-pair record also
 // carries both children's KD boxes (the node region clipped to its
 // triangles' bounds, KDTree.hpp:154-155) as fp16 rounded outward
@@ -296,7 +292,7 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
         uint32_t w0 = r.nw0, w1 = r.nw1;
         int steps = 0;
         while ((w0 >> 30) != 3u) {
-            if (steps == kDescentCap) {       // resume here on the next call
+            if (steps == (BOXES ? MCPT_DESCENT_CAP_GLOBAL : MCPT_DESCENT_CAP)) {       // resume here on the next call
                 r.nw0 = w0;
                 r.nw1 = w1;
                 return false;
@@ -375,8 +371,6 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
         r.lpos = w0 & 0x3FFFFFFFu;
         r.lend = r.lpos + w1;
     }
-#if MCPT_TRI_PAIR
-    static_assert(kTriCap == 2, "paired triangle tests assume a cap of 2");
     // the stack's top slot, read ahead: the pop after this leaf's last tests
     // then needs no LDS round trip of its own (unused if the leaf goes on or
     // the stack is empty -- the slot index is in range either way)
@@ -385,7 +379,10 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
         // both triangles' records are read before either test runs, so the two
         // LDS round trips (leaf ref -> triangle) overlap instead of chaining; a
         // leaf's last single triangle re-reads its own record as the second one
-        // (in bounds: the ref after a leaf section's end is image padding/geoms)
+        // (in bounds: the ref after a leaf section's end is image padding/geoms).
+        // (Leaf records carrying their first two triangle slots inline, with the
+        // next pair prefetched a call ahead, removed the ref round trip but
+        // measured 10.52 vs 10.72 G rays/s: the kernel is issue-bound there.)
         const bool two = r.lend - r.lpos >= 2u;
         const uint32_t k0 = leafs[r.lpos], k1n = leafs[r.lpos + 1u];
         const uint32_t k1 = two ? k1n : k0;
@@ -397,20 +394,8 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
         test_tri_pair(r, a0, a1, a2, k0, b0, b1, b2, k1, two);
         r.lpos += two ? 2u : 1u;
     }
-#else
-    for (uint32_t i = 0; i < kTriCap && r.lpos < r.lend; i++, r.lpos++) {
-        if constexpr (COUNT) c.refs++;
-        MCPT_LANE_USE(tri_w, tri_l, lu);
-        if constexpr (COUNT) c.tests++;
-        test_tri(r, tris, leafs[r.lpos]);
-    }
-#endif
     if (r.lpos < r.lend) return false;        // more triangles in this leaf
-#if MCPT_TRI_PAIR
     return !pop_entry<S, !BOXES>(r, st, stride, spill, spill_stride, &top);
-#else
-    return !pop_entry<S, !BOXES>(r, st, stride, spill, spill_stride);
-#endif
 }
 
 // work unit v (packed owned-pixel index) -> image pixel; false outside the image
