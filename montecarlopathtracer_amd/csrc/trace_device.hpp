@@ -289,14 +289,13 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
                                           uint4* st, int stride, uint4* __restrict__ spill, uint32_t spill_stride,
                                           Counters& c MCPT_LU_PARAM, const uint4* __restrict__ pairs = nullptr) {
     if (r.lpos == r.lend) {                   // between leaves: descend
-        uint32_t w0 = r.nw0, w1 = r.nw1;
+        // the walk advances r.nw0/r.nw1 in place (local copies written back at
+        // the cap cost register moves on every path through the loop)
+        uint32_t& w0 = r.nw0;
+        uint32_t& w1 = r.nw1;
         int steps = 0;
         while ((w0 >> 30) != 3u) {
-            if (steps == (BOXES ? MCPT_DESCENT_CAP_GLOBAL : MCPT_DESCENT_CAP)) {       // resume here on the next call
-                r.nw0 = w0;
-                r.nw1 = w1;
-                return false;
-            }
+            if (steps == (BOXES ? MCPT_DESCENT_CAP_GLOBAL : MCPT_DESCENT_CAP)) return false;   // resume next call
             steps++;
             if constexpr (COUNT) c.inner++;
             MCPT_LANE_USE(desc_w, desc_l, lu);
@@ -362,8 +361,6 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
             if constexpr (BOXES) {
                 if (!(go_far ? far_ok : near_ok)) {   // the chosen child's box is missed: next interval
                     if (!pop_entry<S, !BOXES>(r, st, stride, spill, spill_stride)) return true;
-                    w0 = r.nw0;
-                    w1 = r.nw1;
                 }
             }
         }
