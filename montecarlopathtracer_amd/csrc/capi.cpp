@@ -280,7 +280,7 @@ void build_image(mcpt_scene& s) {
         for (uint32_t i : ord.leaf_order) {
             leaf_begin_new[i] = at;
             for (uint32_t r = 0; r < hs.nodes[i].leaf_count; ++r)
-                refs[at++] = ord.tri_new[hs.leaf_ids[hs.nodes[i].leaf_begin + r]];
+                refs[at++] = 3u * ord.tri_new[hs.leaf_ids[hs.nodes[i].leaf_begin + r]];   // record index
         }
     }
     for (uint32_t i = 0; i < nn; ++i) {

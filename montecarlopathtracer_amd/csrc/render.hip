@@ -213,7 +213,7 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
                 if (r.htri < 0 || depth >= 3 * kp.max_depth || (depth >= kp.max_depth && !qe_roulette(sd, color))) {
                     done = true;
                 } else {
-                    const GpuGeom& g = geoms[__float_as_uint(tris[3 * r.htri + 1].w)];
+                    const GpuGeom& g = geoms[__float_as_uint(tris[r.htri + 1].w)];
                     if (is_emitter(g)) {
                         L = emitted(color, g, 1.0f);
                         done = true;
@@ -228,7 +228,7 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
                 if (r.htri < 0) {
                     done = true;
                 } else {
-                    const uint32_t gi = __float_as_uint(tris[3 * r.htri + 1].w);
+                    const uint32_t gi = __float_as_uint(tris[r.htri + 1].w);
                     const GpuGeom& g = geoms[gi];
                     if (is_emitter(g)) {
                         L = emitted(color, g, kp.illum);
@@ -242,7 +242,7 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
                 }
             } else {
                 if (r.htri >= 0) {
-                    const uint32_t gi = __float_as_uint(tris[3 * r.htri + 1].w);
+                    const uint32_t gi = __float_as_uint(tris[r.htri + 1].w);
                     const GpuGeom& g = geoms[gi];
                     L = emitted(color, g, kp.illum);
                 }

@@ -9,7 +9,9 @@
 //          sibling pair (left, left+1; left is odd in BFS order) is one aligned
 //          16-B record: inner x = axis<<30 | left child, y = split value bits;
 //          leaf x = 3<<30 | first leaf ref, y = count                       8 B
-//   leafs  uint32 KD triangle id per leaf reference                    4 B
+//   leafs  uint32 per leaf reference: the float4 index (3 x slot) of its
+//          triangle's record -- also the index of its normals, and the ray's
+//          hit id (no multiply on the hot path)                           4 B
 //   (scenes too large for LDS: nodes are 48-B sibling-pair records instead,
 //          the two node words + both children's KD boxes as 6 x fp16
 //          rounded outward; the root's record is GpuScene::root_w)        48 B

@@ -186,7 +186,7 @@ __device__ __forceinline__ void test_tri_pair(RayState& r, const float4 A0, cons
 #endif
 }
 __device__ __forceinline__ void test_tri(RayState& r, const float4* __restrict__ tris, uint32_t k) {
-    test_tri_v(r, tris[3 * k], tris[3 * k + 1], tris[3 * k + 2], k);
+    test_tri_v(r, tris[k], tris[k + 1], tris[k + 2], k);
 }
 
 // One resumable traversal iteration: descend to a leaf, test it (two
@@ -383,8 +383,8 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
         const bool two = r.lend - r.lpos >= 2u;
         const uint32_t k0 = leafs[r.lpos], k1n = leafs[r.lpos + 1u];
         const uint32_t k1 = two ? k1n : k0;
-        const float4 a0 = tris[3 * k0], a1 = tris[3 * k0 + 1], a2 = tris[3 * k0 + 2];
-        const float4 b0 = tris[3 * k1], b1 = tris[3 * k1 + 1], b2 = tris[3 * k1 + 2];
+        const float4 a0 = tris[k0], a1 = tris[k0 + 1], a2 = tris[k0 + 2];
+        const float4 b0 = tris[k1], b1 = tris[k1 + 1], b2 = tris[k1 + 2];
         MCPT_LANE_USE(tri_w, tri_l, lu);
         if constexpr (COUNT) c.refs += two ? 2u : 1u;
         if constexpr (COUNT) c.tests += two ? 2u : 1u;
@@ -497,7 +497,7 @@ template <bool QE = false>
 __device__ __forceinline__ void scatter(const GpuGeom& g, const float4* __restrict__ normals, int32_t htri,
                                         float hbeta, float hgamma, float best, int32_t fresnel_kd, uint32_t& sd,
                                         V3& color, V3& o, V3& d) {
-    const float4 n1 = normals[3 * htri], n2 = normals[3 * htri + 1], n3 = normals[3 * htri + 2];
+    const float4 n1 = normals[htri], n2 = normals[htri + 1], n3 = normals[htri + 2];
     scatter_n<QE>(g, n1, n2, n3, hbeta, hgamma, best, fresnel_kd, sd, color, o, d);
 }
 // material class of a geometry for the wavefront's per-material queues

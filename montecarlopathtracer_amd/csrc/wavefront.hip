@@ -278,7 +278,7 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
             // bounce < 3*depth (rtx.hlsl:312), roulette is drawn in shade
             const int32_t lim = kp.mode == kModeQE ? 3 * kp.max_depth : kp.max_depth;
             if (r.htri >= 0 && depth != kNoRay && (int32_t)depth < lim) {
-                const GpuGeom& gm = geoms[__float_as_uint(tris[3 * r.htri + 1].w)];
+                const GpuGeom& gm = geoms[__float_as_uint(tris[r.htri + 1].w)];
                 if (!is_emitter(gm)) cls = material_class(gm);
             }
             if (nslot < count) {
@@ -360,7 +360,7 @@ __global__ void __launch_bounds__(kShadeBlock) wf_shade(const KernelParams kp, c
             // QE: miss / bounce >= 3*depth -> 0; roulette, then emitter -> color*Ka (rtx.hlsl:312-331)
             V3 L = v3(0, 0, 0);
             if (htri >= 0 && depth != kNoRay) {
-                const GpuGeom& gm = geoms[__float_as_uint(tris[3 * htri + 1].w)];
+                const GpuGeom& gm = geoms[__float_as_uint(tris[htri + 1].w)];
                 if (qe) {
                     if ((int32_t)depth < 3 * kp.max_depth) {
                         V3 color = xyz(ps);
@@ -385,7 +385,7 @@ __global__ void __launch_bounds__(kShadeBlock) wf_shade(const KernelParams kp, c
                 nr[3] = make_float4(0, 0, 0, 0);
             } else {
                 c.shades++;
-                const GpuGeom& gm = geoms[__float_as_uint(tris[3 * htri + 1].w)];
+                const GpuGeom& gm = geoms[__float_as_uint(tris[htri + 1].w)];
                 V3 o = xyz(o4), d = xyz(d4);
                 if (qe) scatter<true>(gm, sc.normals, htri, h.y, h.z, h.x, 0, sd, color, o, d);
                 else scatter<false>(gm, sc.normals, htri, h.y, h.z, h.x, kp.fresnel_kd, sd, color, o, d);
