@@ -253,9 +253,7 @@ __device__ __forceinline__ V3 sample_phong(uint32_t& sd, V3 n, V3 in, float ns1)
 // d.z / invlen for Phong and d.z * (1 / invlen) for the hemisphere.
 // Returns the rotated lobe vector (the hemisphere direction, or Phong's half
 // vector before the reflection).
-__device__ __forceinline__ V3 sample_lobe(uint32_t& sd, V3 n, bool phong, float ns1) {
-    float x = rng_next(sd);
-    float y = rng_next(sd);
+__device__ __forceinline__ V3 sample_lobe_u(float x, float y, V3 n, bool phong, float ns1) {
     float cosT, sinT;
     if (phong) {
         cosT = pow_f(x, 1.0f / ns1);
@@ -280,12 +278,16 @@ __device__ __forceinline__ V3 sample_lobe(uint32_t& sd, V3 n, bool phong, float 
     }
     return h;
 }
+__device__ __forceinline__ V3 sample_lobe(uint32_t& sd, V3 n, bool phong, float ns1) {
+    float x = rng_next(sd);
+    float y = rng_next(sd);
+    return sample_lobe_u(x, y, n, phong, ns1);
+}
 // Fresnel: CVMCTracer normalizes only the refracted directions (epsilon-guarded
 // Utils.hpp:27-34; Utils.hpp:97-137); QuinEngine normalizes every output, the
 // mirror and total-internal-reflection branches included (rtx.hlsl:213-251)
 template <bool QE = false>
-__device__ __forceinline__ V3 sample_fresnel(uint32_t& sd, V3 n, V3 in, float Tr, float Ni) {
-    float x = rng_next(sd);
+__device__ __forceinline__ V3 sample_fresnel_u(float x, V3 n, V3 in, float Tr, float Ni) {
     V3 out;
     float ndoti = dot3(in, n);
     Tr = Tr * (1 - pow5_f(1 - fabsf(ndoti)));
@@ -309,6 +311,11 @@ __device__ __forceinline__ V3 sample_fresnel(uint32_t& sd, V3 n, V3 in, float Tr
     }
     if constexpr (QE) normalize_hlsl(out);
     return out;
+}
+template <bool QE = false>
+__device__ __forceinline__ V3 sample_fresnel(uint32_t& sd, V3 n, V3 in, float Tr, float Ni) {
+    float x = rng_next(sd);
+    return sample_fresnel_u<QE>(x, n, in, Tr, Ni);
 }
 
 // -------------------------- ray / triangle ----------------------------------

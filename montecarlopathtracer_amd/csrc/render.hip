@@ -126,7 +126,58 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
 #else
 #define MCPT_STAMP(acc) do {} while (0)
 #endif
+    // Main loop: a shading round for the ready lanes (raised issue priority:
+    // a wave in its short round gets back to traversal sooner while the other
+    // waves' bursts fill the gaps, +0.6%), the work-unit handout for lanes whose
+    // unit is done, the next rays of all of them, then a traversal burst.  The
+    // first round finds every lane needing a unit.  Lanes starting a path (a new
+    // unit's first sample or a unit's next sample) and lanes scattering share
+    // one instruction stream for their two uniforms, the normalize (primary
+    // direction / shading normal) and the root interval, so each runs once per
+    // round however the lanes split (CV mode).
     for (;;) {
+        __builtin_amdgcn_s_setprio(1);
+        bool scat = false, newp = false;   // this lane scatters / starts a path in this round
+        uint32_t gi = 0;                   // geometry of the hit (scatter lanes)
+        if (mode == kReady) {
+            // ---- shading (CUTracer.cu:105-175; QE rtx.hlsl:309-370) ----
+            const bool hit = r.htri >= 0;
+            if (hit) gi = __float_as_uint(tris[r.htri + 1].w);
+            const GpuGeom& g = geoms[gi];
+            bool emit = false;
+            if constexpr (QE) {
+                // miss or bounce >= 3*depth ends the path; roulette from bounce `depth`
+                // on; emitters return color*Ka (no ILLUM)
+                const bool alive = hit && depth < 3 * kp.max_depth &&
+                                   !(depth >= kp.max_depth && !qe_roulette(sd, color));
+                emit = alive && is_emitter(g);
+                scat = alive && !emit;
+            } else {
+                emit = hit && (is_emitter(g) || depth >= kp.max_depth);   // the terminal query collects Ka
+                scat = hit && !emit;
+            }
+            MCPT_STAMP(tm_scatter);
+            if (!scat) {
+                const V3 L = emit ? emitted(color, g, QE ? 1.0f : kp.illum) : v3(0, 0, 0);
+                part = vadd(part, L);
+                s++;
+                if (s == s_end) {
+                    store_part(kp, unit_id, part);
+                    if constexpr (DBG) {
+                        uint32_t* uc = kp.unit_counters + 4 * (size_t)unit_id;
+                        uc[0] = c.rays - c0.rays;
+                        uc[1] = c.inner - c0.inner;
+                        uc[2] = c.leaf - c0.leaf;
+                        uc[3] = c.tests - c0.tests;
+                    }
+                    mode = kNeed;
+                } else {
+                    newp = true;
+                }
+            }
+        }
+        MCPT_STAMP(tm_shade);
+
         // ---- work units: one atomic per wave for every lane that needs one ----
         for (;;) {
             const uint64_t m = __ballot(mode == kNeed);
@@ -167,8 +218,8 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
                     if (s >= s_end) {
                         // sample past spp in a ragged last chunk: nothing to do, take another item
                     } else if (unit_pixel(kp, v, px, py)) {
-                        new_path();
-                        start_ray();
+                        newp = true;
+                        mode = kReady;
                     } else {
                         store_part(kp, unit_id, part);
                     }
@@ -178,7 +229,48 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
         if (!__ballot(mode != kDead)) break;
         MCPT_STAMP(tm_units);
 
-        // ---- traversal burst: until half the wave is ready to shade --------
+        // ---- next rays: scattered rays and the first rays of new paths ----
+        if constexpr (QE) {
+            if (newp) new_path();
+            if (scat) {
+                if constexpr (COUNT) c.shades++;
+                scatter<true>(geoms[gi], sc.normals, r.htri, r.hbeta, r.hgamma, r.best, 0, sd, color, r.o, r.d);
+                depth++;
+            }
+        } else {
+            const bool fres = scat && geoms[gi].Tr > 0;
+            if (newp) sd = path_seed(kp, (uint32_t)py * (uint32_t)kp.width + (uint32_t)px, s);
+            // the lane's next two uniforms (a Fresnel scatter consumes only the first):
+            // the primary ray's jitter (CUTracer.cu:189-190) or the sampler's draws
+            float u1 = 0.0f, u2 = 0.0f;
+            if (scat | newp) {
+                uint32_t s1 = sd;
+                u1 = rng_next(s1);
+                uint32_t s2 = s1;
+                u2 = rng_next(s2);
+                sd = fres ? s1 : s2;
+            }
+            V3 vec = v3(0, 0, 0);
+            if (scat) vec = shading_normal_raw(sc.normals, r.htri, r.hbeta, r.hgamma);
+            if (newp) vec = primary_dir_raw(kp, px, py, u1, u2);
+            if (scat | newp) normalize_cu(vec);
+            if (newp) {
+                r.d = vec;
+                r.o = eye;
+                color = v3(1, 1, 1);
+                depth = 0;
+                if constexpr (COUNT) c.paths++;
+            }
+            if (scat) {
+                if constexpr (COUNT) c.shades++;
+                scatter_u(geoms[gi], vec, u1, u2, r.best, kp.fresnel_kd, color, r.o, r.d);
+                depth++;
+            }
+        }
+        if (scat | newp) start_ray();
+        MCPT_STAMP(tm_shade);
+
+        // ---- traversal burst: until ready_thresh lanes are ready to shade ----
         __builtin_amdgcn_s_setprio(0);
         for (;;) {
 #ifdef MCPT_PHASE_TIMING
@@ -197,79 +289,6 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
             if (!trv || __popcll(rdy) >= kp.ready_thresh) break;
         }
         MCPT_STAMP(tm_trav);
-
-        // ---- shading round for every ready lane (CUTracer.cu:105-175) -------
-        // (and the unit handout after it) at raised issue priority: a wave in
-        // its short shading round gets back to traversal sooner while the
-        // others' LDS-latency-bound bursts fill the gaps (+0.6%; raising the
-        // bursts' priority instead cost 1%)
-        __builtin_amdgcn_s_setprio(1);
-        if (mode == kReady) {
-            bool done = false, cont = false;
-            V3 L = v3(0, 0, 0);
-            if constexpr (QE) {
-                // rtx.hlsl:309-370: miss or bounce >= 3*depth ends the path; roulette
-                // from bounce `depth` on; emitters return color*Ka (no ILLUM)
-                if (r.htri < 0 || depth >= 3 * kp.max_depth || (depth >= kp.max_depth && !qe_roulette(sd, color))) {
-                    done = true;
-                } else {
-                    const GpuGeom& g = geoms[__float_as_uint(tris[r.htri + 1].w)];
-                    if (is_emitter(g)) {
-                        L = emitted(color, g, 1.0f);
-                        done = true;
-                    } else {
-                        if constexpr (COUNT) c.shades++;
-                        scatter<true>(g, sc.normals, r.htri, r.hbeta, r.hgamma, r.best, 0, sd, color, r.o, r.d);
-                        depth++;
-                        cont = true;
-                    }
-                }
-            } else if (depth < kp.max_depth) {
-                if (r.htri < 0) {
-                    done = true;
-                } else {
-                    const uint32_t gi = __float_as_uint(tris[r.htri + 1].w);
-                    const GpuGeom& g = geoms[gi];
-                    if (is_emitter(g)) {
-                        L = emitted(color, g, kp.illum);
-                        done = true;
-                    } else {
-                        if constexpr (COUNT) c.shades++;
-                        scatter(g, sc.normals, r.htri, r.hbeta, r.hgamma, r.best, kp.fresnel_kd, sd, color, r.o, r.d);
-                        depth++;
-                        cont = true;
-                    }
-                }
-            } else {
-                if (r.htri >= 0) {
-                    const uint32_t gi = __float_as_uint(tris[r.htri + 1].w);
-                    const GpuGeom& g = geoms[gi];
-                    L = emitted(color, g, kp.illum);
-                }
-                done = true;
-            }
-            MCPT_STAMP(tm_scatter);
-            if (done) {
-                part = vadd(part, L);
-                s++;
-                if (s == s_end) {
-                    store_part(kp, unit_id, part);
-                    if constexpr (DBG) {
-                        uint32_t* uc = kp.unit_counters + 4 * (size_t)unit_id;
-                        uc[0] = c.rays - c0.rays;
-                        uc[1] = c.inner - c0.inner;
-                        uc[2] = c.leaf - c0.leaf;
-                        uc[3] = c.tests - c0.tests;
-                    }
-                    mode = kNeed;
-                } else {
-                    new_path();
-                    cont = true;
-                }
-            }
-            if (cont) start_ray();   // scattered ray or next sample's primary ray
-        }
-        MCPT_STAMP(tm_shade);
     }
 
 #ifdef MCPT_PHASE_TIMING

@@ -426,6 +426,25 @@ __device__ __forceinline__ void primary_ray_sd(const KernelParams& kp, int px, i
     normalize_cu(wr);
     dir = wr;
 }
+// primary_ray_sd's direction before its normalize, from its two jitter
+// uniforms u1, u2 (the main loop normalizes it together with the shading
+// normals of the scattering lanes)
+__device__ __forceinline__ V3 primary_dir_raw(const KernelParams& kp, int px, int py, float u1, float u2) {
+    const float biasx = (float)(uint32_t)px + (u1 * 2.0f - 1.0f);
+    const float biasy = (float)(uint32_t)py + (u2 * 2.0f - 1.0f);
+    const double th = (double)kp.tan_half_fov;
+    const double W = (double)(uint32_t)kp.width;
+    const double qx = kp.inv_w_pow2 != 0.0 ? 2.0 * (double)biasx * kp.inv_w_pow2 : 2.0 * (double)biasx / W;
+    const double qy = kp.inv_w_pow2 != 0.0 ? 2.0 * (double)biasy * kp.inv_w_pow2 : 2.0 * (double)biasy / W;
+    const float idx = (float)((qx - 1) * th);
+    const float idy = (float)((kp.h_over_w - qy) * th);
+    const float idz = -1.0f;
+    V3 wr;
+    wr.x = kp.right[0] * idx + kp.up[0] * idy - kp.fwd[0] * idz;
+    wr.y = kp.right[1] * idx + kp.up[1] * idy - kp.fwd[1] * idz;
+    wr.z = kp.right[2] * idx + kp.up[2] * idy - kp.fwd[2] * idz;
+    return wr;
+}
 // primary ray of sample s of pixel (px, py)
 __device__ __forceinline__ void primary_ray(const KernelParams& kp, uint32_t pix, int px, int py, uint32_t s,
                                             uint32_t& sd, V3& dir) {
@@ -489,6 +508,37 @@ __device__ __forceinline__ void scatter_n(const GpuGeom& g, float4 n1, float4 n2
     }
     // hitPoint = pos + t*dir at the accepted t (CUTracer.cu:89-91), then
     // pos = hitPoint + dir*0.01 (:134,143,159)
+    const V3 hp = v3(o.x + best * d.x, o.y + best * d.y, o.z + best * d.z);
+    o = vadd(hp, vscale(dir, 0.01f));
+    d = dir;
+}
+// The shading normal before its normalize (CUTracer.cu:120-126)
+__device__ __forceinline__ V3 shading_normal_raw(const float4* __restrict__ normals, int32_t htri, float hbeta,
+                                                 float hgamma) {
+    const float4 n1 = normals[htri], n2 = normals[htri + 1], n3 = normals[htri + 2];
+    return vadd(vadd(vscale(v3(n1.x, n1.y, n1.z), 1.0f - hbeta - hgamma), vscale(v3(n2.x, n2.y, n2.z), hbeta)),
+                vscale(v3(n3.x, n3.y, n3.z), hgamma));
+}
+// scatter_n (CVMCTracer mode) from the normalized shading normal and the
+// lane's next two uniforms, already drawn (u2 unused by a Fresnel material)
+__device__ __forceinline__ void scatter_u(const GpuGeom& g, V3 nrm, float u1, float u2, float best,
+                                          int32_t fresnel_kd, V3& color, V3& o, V3& d) {
+    V3 dir = d;
+    if (g.Tr > 0) {
+        dir = sample_fresnel_u<false>(u1, nrm, dir, g.Tr, g.Ni);
+        if (fresnel_kd) color = v3(color.x * g.Kd[0], color.y * g.Kd[1], color.z * g.Kd[2]);
+    } else {
+        const bool ph = g.Ns > 1;
+        const bool flip = dot3(dir, nrm) > 0;
+        const V3 h = sample_lobe_u(u1, u2, nrm, ph, (float)(g.Ns_u + 1u));
+        if (ph) {
+            dir = vsub(dir, vscale(vscale(h, dot3(dir, h)), 2.0f));
+            color = v3(color.x * g.Ks[0], color.y * g.Ks[1], color.z * g.Ks[2]);
+        } else {
+            color = v3(color.x * g.Kd[0], color.y * g.Kd[1], color.z * g.Kd[2]);
+            dir = flip ? v3(-h.x, -h.y, -h.z) : h;
+        }
+    }
     const V3 hp = v3(o.x + best * d.x, o.y + best * d.y, o.z + best * d.z);
     o = vadd(hp, vscale(dir, 0.01f));
     d = dir;
