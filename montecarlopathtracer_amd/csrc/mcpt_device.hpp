@@ -253,6 +253,9 @@ __device__ __forceinline__ V3 sample_phong(uint32_t& sd, V3 n, V3 in, float ns1)
 // d.z / invlen for Phong and d.z * (1 / invlen) for the hemisphere.
 // Returns the rotated lobe vector (the hemisphere direction, or Phong's half
 // vector before the reflection).
+#ifndef MCPT_FRESNEL_MERGED
+#define MCPT_FRESNEL_MERGED 1
+#endif
 __device__ __forceinline__ V3 sample_lobe_u(float x, float y, V3 n, bool phong, float ns1) {
     float cosT, sinT;
     if (phong) {
@@ -288,9 +291,38 @@ __device__ __forceinline__ V3 sample_lobe(uint32_t& sd, V3 n, bool phong, float 
 // mirror and total-internal-reflection branches included (rtx.hlsl:213-251)
 template <bool QE = false>
 __device__ __forceinline__ V3 sample_fresnel_u(float x, V3 n, V3 in, float Tr, float Ni) {
-    V3 out;
     float ndoti = dot3(in, n);
     Tr = Tr * (1 - pow5_f(1 - fabsf(ndoti)));
+#if MCPT_FRESNEL_MERGED
+    // Entering (ndoti <= 0) and leaving refraction in one body: each lane forms
+    // its branch's alpha terms -- the entering branch's six divisions by Ni as
+    // RN(a * r) with one shared reciprocal r of Ni (bit-identical to IEEE a / Ni,
+    // see recip_shared) -- then one sqrt, one n*alpha + in' and one normalize.
+    const bool enter = ndoti <= 0;
+    const float w = 1 - ndoti * ndoti;
+    float a0, rad;
+    V3 ins;
+    if (enter) {
+        const double rn = recip_shared(Ni);
+        a0 = div_shared(-ndoti, rn);                       // -ndoti / Ni
+        rad = 1 - div_shared(div_shared(w, rn), rn);       // 1 - (1 - ndoti^2) / Ni / Ni
+        ins = v3(div_shared(in.x, rn), div_shared(in.y, rn), div_shared(in.z, rn));   // in / Ni
+    } else {
+        a0 = -ndoti * Ni;
+        rad = 1 - w * Ni * Ni;                             // `test`: < 0 is total internal reflection
+        ins = vscale(in, Ni);
+    }
+    V3 out;
+    if (x < Tr && (enter || !(rad < 0))) {
+        const float sq = sqrt_rn(rad);
+        const float alpha = enter ? a0 - sq : a0 + sq;
+        out = vadd(vscale(n, alpha), ins);
+        if constexpr (!QE) normalize_cu(out);
+    } else {
+        out = vsub(in, vscale(vscale(n, dot3(in, n)), 2.0f));
+    }
+#else
+    V3 out;
     if (x < Tr) {
         if (ndoti <= 0) {
             float alpha = -ndoti / Ni - sqrt_rn(1 - (1 - ndoti * ndoti) / Ni / Ni);
@@ -309,6 +341,7 @@ __device__ __forceinline__ V3 sample_fresnel_u(float x, V3 n, V3 in, float Tr, f
     } else {
         out = vsub(in, vscale(vscale(n, dot3(in, n)), 2.0f));
     }
+#endif
     if constexpr (QE) normalize_hlsl(out);
     return out;
 }

@@ -227,6 +227,7 @@ __global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
             }
         }
         if (!__ballot(mode != kDead)) break;
+        if constexpr (!DBG) bound_counters<COUNT>(c, kp.stats);   // (DBG: per-unit deltas of c)
         MCPT_STAMP(tm_units);
 
         // ---- next rays: scattered rays and the first rays of new paths ----

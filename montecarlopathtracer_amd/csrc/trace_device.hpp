@@ -597,20 +597,34 @@ struct SlotCursor {
     }
 };
 
-// counters: wave reduction, one atomic per wave per counter
+// counters: wave reduction in 64 bits (64 lanes of 32-bit counts may exceed
+// 2^32), one atomic per wave per counter
 __device__ __forceinline__ void flush_counters(const Counters& c, unsigned long long* stats) {
-    uint32_t vals[8] = {c.rays, c.paths, c.inner, c.leaf, c.refs, c.tests, c.shades, c.spills};
+    const uint32_t vals[8] = {c.rays, c.paths, c.inner, c.leaf, c.refs, c.tests, c.shades, c.spills};
+    unsigned long long sums[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) {
-        uint32_t x = vals[i];
+        unsigned long long x = vals[i];
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
-        vals[i] = x;
+        sums[i] = x;
     }
     if ((threadIdx.x & 63u) == 0) {
 #pragma unroll
         for (int i = 0; i < 8; i++)
-            if (vals[i]) atomicAdd(stats + i, (unsigned long long)vals[i]);
+            if (sums[i]) atomicAdd(stats + i, sums[i]);
+    }
+}
+// Per-lane counts are 32-bit: a wave flushes them (and restarts from 0) once
+// any lane's largest count passes 2^30, so no count can wrap however long a
+// persistent wave runs (a C4-mesh frame at 4096 spp reaches ~2^21 per lane).
+// Wave-uniform; the check is one compare and a ballot per main-loop round.
+template <bool COUNT>
+__device__ __forceinline__ void bound_counters(Counters& c, unsigned long long* stats) {
+    const uint32_t big = COUNT ? c.inner : c.rays;   // the fastest-growing count of the kernel
+    if (__ballot(big > (1u << 30))) {
+        flush_counters(c, stats);
+        c = Counters{0, 0, 0, 0, 0, 0, 0, 0};
     }
 }
 
