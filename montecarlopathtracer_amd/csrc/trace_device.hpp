@@ -38,6 +38,20 @@ __device__ __forceinline__ void lane_use(unsigned long long& w, unsigned long lo
 #define MCPT_LANE_USE(wf, lf, acc) do {} while (0)
 #endif
 
+// IEEE maxNum / minNum as one instruction: a quiet-NaN operand yields the
+// other one.  (fmaxf/fminf compile to the same instruction plus a canonicalizing
+// v_max of each input, which only matters for signalling NaNs -- the operands
+// here are products and stored interval ends, never sNaN.)
+__device__ __forceinline__ float max_qnan(float a, float b) {
+    float r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float min_qnan(float a, float b) {
+    float r;
+    asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
 __device__ __forceinline__ float sel3(int a, float x, float y, float z) {
     return a == 0 ? x : (a == 1 ? y : z);
 }
@@ -312,12 +326,18 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
             const int a = (int)(w0 >> 30);
             const float sv = __uint_as_float(w1);
             const float oa = sel3(a, r.o.x, r.o.y, r.o.z);
-            const float da = sel3(a, r.d.x, r.d.y, r.d.z);
             const float ia = sel3(a, r.ix, r.iy, r.iz);
             const float t = (sv - oa) * ia;
-            const bool below = (oa < sv) | ((oa == sv) & (da <= 0.0f));
+            // near side: below the plane, or on it and heading down; pp = ray inside
+            // the plane (both children).  Only an origin exactly on the plane needs
+            // the direction, so its select and tests sit in a rarely taken branch.
+            bool below = oa < sv, pp = false;
+            if (__builtin_expect(oa == sv, 0)) {
+                const float da = sel3(a, r.d.x, r.d.y, r.d.z);
+                below = da <= 0.0f;
+                pp = da == 0.0f;
+            }
             // if/else chain of the oracle, evaluated branch-free
-            const bool pp = (da == 0.0f) & (oa == sv);                  // ray inside the plane: both
             const float te = t * kEpsHi;
             const bool no = !(t > 0.0f) | (t > r.tmax);                 // near child only
             const bool fo = te < r.tmin;                                // far child only
@@ -334,7 +354,9 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
             }
             const uint32_t f0 = below ? pr.z : pr.x, f1 = below ? pr.w : pr.y;     // far child record
             if (push_it) {
-                const float plo = pp ? r.tmin : (t > r.tmin ? t : r.tmin);
+                // pp ? tmin : max(t, tmin) without the select: a pp lane's t is
+                // (+0) * (+-inf) = NaN (da = +-0, oa == sv), and max returns tmin
+                const float plo = max_qnan(t, r.tmin);
                 uint4* slot = st + (r.sp & (S - 1)) * stride;
                 if constexpr (!BOXES) {
                     if (r.sp - r.lo == S) {           // LDS part full: its oldest entry (same slot) to memory
@@ -348,8 +370,8 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
                 }
                 *slot = make_uint4(f0, f1, __float_as_uint(plo), __float_as_uint(r.tmax));
                 r.sp++;
-                if constexpr (!BOXES)                                   // here push_it & !pp == both
-                    if (!pp) r.tmax = te < r.tmax ? te : r.tmax;
+                if constexpr (!BOXES)                // here push_it & !pp == both; te = NaN for pp
+                    r.tmax = min_qnan(te, r.tmax);
             }
             if constexpr (BOXES)                                        // the near child's interval,
                 if (both) r.tmax = te < r.tmax ? te : r.tmax;           // pushed far or not
