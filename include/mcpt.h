@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define MCPT_ABI_VERSION 4
+#define MCPT_ABI_VERSION 5
 
 enum {
     MCPT_OK = 0,
@@ -218,6 +218,15 @@ int mcpt_render_unit_counters(mcpt_scene* s, const mcpt_render_params* p, float*
 /* number of output pixels a (sharded) render writes, and their (x,y) list */
 int64_t mcpt_shard_pixel_count(const mcpt_render_params* p);
 int mcpt_shard_pixels(const mcpt_render_params* p, int32_t* xy);      /* count*2 */
+/* Closest hit of n caller-given rays on the scene's device, the reference's
+ * intersect() (CUTracer.cu:44-96) through the traversal the renders use (the
+ * ordered KD walk; scenes in global memory with the child-box cull):
+ * o, d = n*3 floats (host); tri_out[i] = kd triangle id (scene_copy_kd's
+ * numbering) or -1; hit_out = n*3 floats beta, gamma, t (t = 0 on a miss);
+ * t_max = the initial closest t (FLT_MAX in CVMCTracer, 10000 in QuinEngine).
+ * stats (may be NULL): rays, inner/leaf visits, leaf refs, tri tests.       */
+int mcpt_intersect(mcpt_scene* s, int64_t n, const float* o, const float* d, float t_max,
+                   int32_t* tri_out, float* hit_out, mcpt_render_stats* stats);
 /* reserve device workspace for p so mcpt_render_device allocates nothing
  * (required before hipGraph capture).  Megakernel workspace per render:
  * partial sums 16 B x pixels x ceil(spp/chunk), the tail-split buffer (16 B

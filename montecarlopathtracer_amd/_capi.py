@@ -21,7 +21,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MCPT_LIB_PATH") or os.path.join(_HERE, "lib", "libmcpt.so")
 
 MCPT_OK = 0
-ABI_VERSION = 4
+ABI_VERSION = 5
 MODE_CVMCTRACER = 0
 MODE_QUINENGINE = 1
 PIPELINE_MEGAKERNEL = 0
@@ -110,6 +110,8 @@ _SIGS = {
     "mcpt_render_unit_counters": (C.c_int, [_vp, C.POINTER(RenderParamsC), C.POINTER(C.c_float),
                                             C.POINTER(C.c_uint32)]),
     "mcpt_render_stats_read": (C.c_int, [_vp, C.POINTER(RenderStats)]),
+    "mcpt_intersect": (C.c_int, [_vp, C.c_int64, C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_float,
+                                 C.POINTER(C.c_int32), C.POINTER(C.c_float), C.POINTER(RenderStats)]),
     "mcpt_shard_pixel_count": (C.c_int64, [C.POINTER(RenderParamsC)]),
     "mcpt_shard_pixels": (C.c_int, [C.POINTER(RenderParamsC), C.POINTER(C.c_int32)]),
     "mcpt_scene_reserve": (C.c_int, [_vp, C.POINTER(RenderParamsC)]),

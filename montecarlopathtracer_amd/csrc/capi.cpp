@@ -1022,6 +1022,54 @@ int mcpt_render(mcpt_scene* s, const mcpt_render_params* p, float* fb_rgb, mcpt_
     return render_sync(s, p, fb_rgb, stats, nullptr);
 }
 
+int mcpt_intersect(mcpt_scene* s, int64_t n, const float* o, const float* d, float t_max, int32_t* tri_out,
+                   float* hit_out, mcpt_render_stats* stats) {
+    return guarded([&]() -> int {
+        if (!s || n < 0 || (n && (!o || !d || !tri_out || !hit_out))) return fail(MCPT_E_INVALID, "NULL argument");
+        if (!s->on_device) return fail(MCPT_E_INVALID, "scene was created host-only");
+        if (n >= (int64_t(1) << 31) / 3) return fail(MCPT_E_UNSUPPORTED, "too many rays for one call");
+        set_device(*s);
+        mcpt_render_stats st;
+        std::memset(&st, 0, sizeof st);
+        st.devices = 1;
+        if (n) {
+            const size_t N = static_cast<size_t>(n);
+            // one allocation: o, d, hits (3 floats each), slots, counters, then the
+            // 16-B aligned stack spill area (32 entries per ray)
+            const size_t stats_off = (N * 40 + 15) & ~size_t(15), spill_off = stats_off + 64;
+            char* buf = nullptr;
+            HIP_TRY(hipMalloc(reinterpret_cast<void**>(&buf), spill_off + N * 32 * 16));
+            struct Free { char* p; ~Free() { (void)hipFree(p); } } guard{buf};
+            mcpt::QueryParams q{};
+            q.scene = s->gpu;
+            q.o = reinterpret_cast<float*>(buf);
+            q.d = q.o + 3 * N;
+            q.hit = reinterpret_cast<float*>(buf) + 6 * N;
+            q.slot = reinterpret_cast<int32_t*>(buf + 36 * N);
+            q.stats = reinterpret_cast<unsigned long long*>(buf + stats_off);
+            q.spill = reinterpret_cast<uint4*>(buf + spill_off);
+            q.n = static_cast<uint32_t>(n);
+            q.best_init = t_max;
+            HIP_TRY(hipMemcpy(buf, o, N * 12, hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(buf + N * 12, d, N * 12, hipMemcpyHostToDevice));
+            HIP_TRY(hipMemset(q.stats, 0, 64));
+            HIP_TRY(mcpt::launch_query(q, nullptr));
+            HIP_TRY(hipDeviceSynchronize());
+            std::vector<int32_t> slot(N);
+            unsigned long long c[8];
+            HIP_TRY(hipMemcpy(slot.data(), q.slot, N * 4, hipMemcpyDeviceToHost));
+            HIP_TRY(hipMemcpy(hit_out, q.hit, N * 12, hipMemcpyDeviceToHost));
+            HIP_TRY(hipMemcpy(c, q.stats, 64, hipMemcpyDeviceToHost));
+            for (size_t i = 0; i < N; ++i)
+                tri_out[i] = slot[i] < 0 ? -1 : static_cast<int32_t>(s->tri_order[static_cast<size_t>(slot[i])]);
+            st.rays = c[0]; st.inner_visits = c[2]; st.leaf_visits = c[3]; st.leaf_refs = c[4];
+            st.tri_tests = c[5]; st.stack_spills = c[7];
+        }
+        if (stats) *stats = st;
+        return MCPT_OK;
+    });
+}
+
 int mcpt_render_unit_counters(mcpt_scene* s, const mcpt_render_params* p, float* fb_rgb, uint32_t* unit_counters) {
     if (!unit_counters) return fail(MCPT_E_INVALID, "unit_counters is NULL");
     return render_sync(s, p, fb_rgb, nullptr, unit_counters);

@@ -51,7 +51,9 @@ __device__ __forceinline__ void store_part(const KernelParams& kp, uint32_t id, 
 }
 
 template <bool IN_LDS, int S, int BLOCK, bool DBG, bool QE, bool COUNT>
-__global__ void __launch_bounds__(BLOCK) path_kernel(const KernelParams kp) {
+// counting kernels of the global layout are held to 4 waves per SIMD (128 VGPRs)
+// by the launch bound; the lean (timed) kernels fit without it
+__global__ void __launch_bounds__(BLOCK, (!IN_LDS && COUNT) ? 4 : 1) path_kernel(const KernelParams kp) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = (int)threadIdx.x;
     const int lane = tid & 63;
@@ -374,6 +376,44 @@ __global__ void __launch_bounds__(256) gather_kernel(const GatherParams g) {
                              g.mode);
 }
 
+// Closest-hit batch (mcpt_intersect): the reference's intersect()
+// (CUTracer.cu:44-96) for caller-given rays, through the traversal the path
+// kernel runs -- trav_iter on the scene image in global memory, the stack's
+// top entries in LDS -- one ray per lane.  Output per ray: the triangle's
+// image slot (-1: miss) and (beta, gamma, t).  Lanes past n run a dummy ray
+// so every lane reaches the wave-level counter flush.
+template <bool BOXES, int S>
+__global__ void __launch_bounds__(kQueryBlock) query_kernel(const QueryParams q) {
+    __shared__ uint4 stk[S * kQueryBlock];
+    const GpuScene& sc = q.scene;
+    const int tid = (int)threadIdx.x;
+    const uint32_t i = blockIdx.x * kQueryBlock + (uint32_t)tid;
+    const bool live = i < q.n;
+    const float4* tris = reinterpret_cast<const float4*>(sc.image + sc.off_tris);
+    const uint2* nodes = reinterpret_cast<const uint2*>(sc.image + sc.off_nodes) + 1;
+    const uint32_t* leafs = reinterpret_cast<const uint32_t*>(sc.image + sc.off_leafs);
+    const uint4* pairs = reinterpret_cast<const uint4*>(sc.image + sc.off_nodes);
+    Counters c = {0, 0, 0, 0, 0, 0, 0, 0};
+#ifdef MCPT_PHASE_TIMING
+    LaneUse lu = {0, 0, 0, 0, 0, 0};
+#endif
+    RayState r;
+    r.o = live ? v3(q.o[3 * i], q.o[3 * i + 1], q.o[3 * i + 2]) : v3(0, 0, 0);
+    r.d = live ? v3(q.d[3 * i], q.d[3 * i + 1], q.d[3 * i + 2]) : v3(0, 0, 1);
+    if (live) c.rays++;
+    if (begin_ray(r, sc, q.best_init) && live)
+        while (!trav_iter<S, BOXES, true>(r, tris, nodes, leafs, stk + tid, kQueryBlock, q.spill + i, q.n,
+                                          c MCPT_LU_ARG, pairs)) {
+        }
+    if (live) {
+        q.slot[i] = r.htri < 0 ? -1 : r.htri / 3;
+        q.hit[3 * i] = r.hbeta;
+        q.hit[3 * i + 1] = r.hgamma;
+        q.hit[3 * i + 2] = r.htri < 0 ? 0.0f : r.best;
+    }
+    flush_counters(c, q.stats);
+}
+
 template <bool IN_LDS, int S, int BLOCK>
 hipError_t launch_path(const KernelParams& kp, int grid, size_t lds, hipStream_t st) {
     const bool qe = kp.mode == kModeQE;
@@ -436,6 +476,16 @@ void read_lane_use(unsigned long long out[6]) {   // megakernel lane-use counter
 
 hipError_t launch_reduce(const KernelParams& kp, float4* fb, hipStream_t st) {
     hipLaunchKernelGGL(reduce_kernel, dim3((kp.npix_local + 255u) / 256u), dim3(256), 0, st, kp, fb);
+    return hipGetLastError();
+}
+
+hipError_t launch_query(const QueryParams& q, hipStream_t st) {
+    if (!q.n) return hipSuccess;
+    const dim3 grid((q.n + kQueryBlock - 1) / kQueryBlock);
+    if (q.scene.node_boxes)
+        hipLaunchKernelGGL((query_kernel<true, 8>), grid, dim3(kQueryBlock), 0, st, q);
+    else
+        hipLaunchKernelGGL((query_kernel<false, 4>), grid, dim3(kQueryBlock), 0, st, q);
     return hipGetLastError();
 }
 

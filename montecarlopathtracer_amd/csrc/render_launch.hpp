@@ -124,6 +124,22 @@ struct GatherParams {
     int32_t mode;
 };
 
+// Closest-hit batch (mcpt_intersect, render.hip query_kernel): rays i < n,
+// origins / directions as 3 floats each; out slot[i] = the hit triangle's image
+// slot (-1 miss), hit[3i..] = beta, gamma, t; spill = [32][n] stack entries
+constexpr int kQueryBlock = 256;
+struct QueryParams {
+    GpuScene scene;
+    const float* o;
+    const float* d;
+    int32_t* slot;
+    float* hit;
+    uint4* spill;
+    unsigned long long* stats;           // 8 counters (Counters order)
+    uint32_t n;
+    float best_init;
+};
+
 // Wavefront pipeline workspace (wavefront.hip).  One batch = samples
 // [s_begin, s_begin + ns) of chunk `chunk` for owned pixels [v0, v0 + nb);
 // path id pid = s_local * nb + (v - v0).  The batch is cut into `nseg`
@@ -161,6 +177,7 @@ hipError_t launch_render(const KernelParams& kp, int cus, hipStream_t st, hipEve
                          hipEvent_t ev2, float4* fb, int* variant_out);
 hipError_t launch_reduce(const KernelParams& kp, float4* fb, hipStream_t st);
 hipError_t launch_gather(const GatherParams& g, hipStream_t st);
+hipError_t launch_query(const QueryParams& q, hipStream_t st);
 #ifdef MCPT_PHASE_TIMING
 void read_lane_use(unsigned long long out[6]);      // diagnostic build only: megakernel
 void read_lane_use_wf(unsigned long long out[6]);   // wavefront extend

@@ -290,6 +290,22 @@ class Scene:
         check(lib().mcpt_render(self.handle, C.byref(params.to_c()), _fptr(fb), C.byref(st)))
         return fb, st.as_dict()
 
+    def intersect(self, o: np.ndarray, d: np.ndarray, t_max: float = 3.402823466e38):
+        """Closest hits of rays (origins o, directions d: (n, 3) float32) on the
+        device (CUTracer.cu:44-96 through the render traversal): (kd triangle id
+        or -1, (n, 3) beta gamma t, counters)."""
+        o = np.ascontiguousarray(o, np.float32).reshape(-1, 3)
+        d = np.ascontiguousarray(d, np.float32).reshape(-1, 3)
+        if o.shape != d.shape:
+            raise McptError(-1, "o and d must have the same shape")
+        n = o.shape[0]
+        tri = np.zeros(n, np.int32)
+        hit = np.zeros((n, 3), np.float32)
+        st = RenderStats()
+        check(lib().mcpt_intersect(self.handle, n, _fptr(o), _fptr(d), C.c_float(t_max),
+                                   tri.ctypes.data_as(C.POINTER(C.c_int32)), _fptr(hit), C.byref(st)))
+        return tri, hit, st.as_dict()
+
     def render_unit_counters(self, params: RenderParams):
         """Synchronous render returning (fb, per-unit counters (units, 4): rays, inner, leaf, tests)."""
         n = params.output_pixels()
