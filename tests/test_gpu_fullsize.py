@@ -1,6 +1,8 @@
 """GPU path at BASELINE sizes, through size-independent properties, plus the
 statistical pin against the reference's own 1000-spp render.
 
+* 512x512 @ 16 spp (BASELINE configs[0], C1) as a whole frame: bit-identical
+  to the CPU oracle, counters equal.
 * 1024x1024 @ 1024 spp (BASELINE configs[1]): rendering the 8 interleaved
   tile shards (configs[2]'s partition) and reassembling them reproduces the
   single-GPU image bit for bit; a second render is bit-identical (determinism);
@@ -54,6 +56,23 @@ def test_fullsize_shards_and_determinism(mcpt, scene01):
     torch.cuda.synchronize()
     scene01.stats()
     assert torch.equal(got[:, :3], full[:, :3])
+
+
+def test_c1_full_frame_bit_identical_to_oracle(mcpt, oracle_mod, scene01):
+    """BASELINE configs[0] (C1: 512x512, 16 spp, the reference's CPU-runnable
+    case) as one whole frame: the device image equals the CPU oracle's ordered
+    walk bit for bit, with equal ray / path / visit / test / shade counts
+    (~14 M closest-hit queries)."""
+    W = H = 512
+    p = mcpt.RenderParams(width=W, height=H, spp=16)
+    img, st = scene01.render(p)
+    o = oracle_mod.Scene(mcpt.scene_path("scene01"))
+    ref, rc = o.render(oracle_mod.RenderParams(width=W, height=H, spp=16, spp_chunk=p.spp_chunk,
+                                               traversal=oracle_mod.KD_ORDERED, threads=16))
+    assert np.array_equal(img.view(np.uint32), ref.view(np.uint32)), float(np.abs(img - ref).max())
+    for k in ("rays", "paths", "inner_visits", "leaf_visits", "leaf_refs", "tri_tests", "shades"):
+        assert st[k] == rc[k], (k, st[k], rc[k])
+    assert st["rays"] > 1.3e7
 
 
 def test_fullsize_pipelines_agree(mcpt, scene01):
