@@ -153,10 +153,10 @@ struct WfCounters {                      // per (bounce, segment), 8 words
     uint32_t pad[3];
 };
 struct WfParams {
-    // ray queue b: one 64-B record per slot, {o.xyz pid} {d.xyz depth}
-    // {t beta gamma htri} {throughput.xyz rng}: extend reads the first half
-    // and fills the hit, shade reads the whole record with one gather
-    float4* q[2];                        // [slot_stride][4]
+    // ray queue b: four float4 streams of slot_stride entries (SoA):
+    // {o.xyz pid} {d.xyz depth} {t beta gamma htri} {throughput.xyz rng};
+    // extend reads streams 0-1 and writes stream 2, shade reads all four
+    float4* q[2];                        // [4][slot_stride]
     uint32_t* cls_list;                  // [4][capacity] slots per material class
     float4* radiance;                    // path radiance per pid                   [capacity]
     WfCounters* cnt;                     // [max_depth + 2][nseg]

@@ -58,6 +58,22 @@ __device__ __forceinline__ float opaque(float x) {
     return y;
 }
 __device__ __forceinline__ float4 pack(V3 v, uint32_t w) { return make_float4(v.x, v.y, v.z, __uint_as_float(w)); }
+
+// Queue layout: field k of slot j (0 {o, pid}, 1 {d, depth}, 2 hit {t, beta,
+// gamma, htri}, 3 {throughput, rng}).  SoA (default): four float4 streams of
+// slot_stride entries each -- extend's ray reads and hit writes are dense
+// 16-B lane streams; AoS: one 64-B record per slot.
+#ifndef MCPT_WF_SOA
+#define MCPT_WF_SOA 1
+#endif
+__device__ __forceinline__ size_t qf(uint32_t slot, uint32_t k, uint32_t stride) {
+#if MCPT_WF_SOA
+    return (size_t)k * stride + slot;
+#else
+    (void)stride;
+    return 4u * (size_t)slot + k;
+#endif
+}
 __device__ __forceinline__ V3 xyz(float4 v) { return v3(v.x, v.y, v.z); }
 
 // Group k of block b (b-th run of nseg consecutive groups) -> its segment:
@@ -108,13 +124,13 @@ __global__ void __launch_bounds__(kGenBlock) wf_generate(const KernelParams kp, 
                 primary_ray_qe(kp, pix, px, py, wf.s_begin + s_local, sd, o, d);
             else
                 primary_ray(kp, pix, px, py, wf.s_begin + s_local, sd, d);
-            wf.q[0][4u * slot + 3u] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(sd));
+            wf.q[0][qf(slot, 3, wf.slot_stride)] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(sd));
             c.paths++;
             c.rays++;
             depth = 0;
         }
-        wf.q[0][4u * slot] = pack(o, pid);
-        wf.q[0][4u * slot + 1u] = pack(d, depth);
+        wf.q[0][qf(slot, 0, wf.slot_stride)] = pack(o, pid);
+        wf.q[0][qf(slot, 1, wf.slot_stride)] = pack(d, depth);
     }
     flush_counters(c, kp.stats);
 }
@@ -203,7 +219,8 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
     uint4* spill = kp.spill + (blockIdx.x * BLOCK + (uint32_t)tid);
     const uint32_t spill_stride = kp.total_lanes;
     const size_t seg0 = (size_t)g * wf.seg;
-    float4* qr = wf.q[wf.bounce & 1] + 4u * seg0;          // this segment's records
+    float4* qb = wf.q[wf.bounce & 1];                      // this bounce's queue
+    const uint32_t qs = wf.slot_stride;
 
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0};
 #ifdef MCPT_PHASE_TIMING
@@ -238,8 +255,8 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
 #else
 #define WF_STAMP(acc) do {} while (0)
 #endif
-    if (slot < count) start(qr[4u * slot], qr[4u * slot + 1u]);
-    if (nslot < count) { no4 = qr[4u * nslot]; nd4 = qr[4u * nslot + 1u]; }
+    if (slot < count) start(qb[qf(seg0 + slot, 0, qs)], qb[qf(seg0 + slot, 1, qs)]);
+    if (nslot < count) { no4 = qb[qf(seg0 + nslot, 0, qs)]; nd4 = qb[qf(seg0 + nslot, 1, qs)]; }
     WF_STAMP(tm_setup);
     for (;;) {
         // ---- traversal burst until enough lanes are done ---------------------
@@ -287,7 +304,7 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
             } else {
                 mode = kDead;
             }
-            qr[4u * fslot + 2u] = hrec;
+            qb[qf(seg0 + fslot, 2, qs)] = hrec;
         }
 #pragma unroll
         for (uint32_t k = 0; k < 4; k++)
@@ -297,7 +314,7 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
         const uint32_t ns = cur_chunk.take(want, lcnt + 4);
         if (want) {
             nslot = ns;
-            if (nslot < count) { no4 = qr[4u * nslot]; nd4 = qr[4u * nslot + 1u]; }
+            if (nslot < count) { no4 = qb[qf(seg0 + nslot, 0, qs)]; nd4 = qb[qf(seg0 + nslot, 1, qs)]; }
         }
         WF_STAMP(tm_hand);
         if (!__ballot(mode != kDead)) break;
@@ -340,8 +357,9 @@ __global__ void __launch_bounds__(kShadeBlock) wf_shade(const KernelParams kp, c
     const float4* tris = reinterpret_cast<const float4*>(sc.image + sc.off_tris);
     const GpuGeom* geoms = reinterpret_cast<const GpuGeom*>(sc.image + sc.off_geoms);
     const size_t seg0 = (size_t)g * wf.seg;
-    const float4* qr = wf.q[wf.bounce & 1] + 4u * seg0;
-    float4* qr2 = wf.q[(wf.bounce + 1) & 1] + 4u * seg0;
+    const float4* qb = wf.q[wf.bounce & 1];
+    float4* qb2 = wf.q[(wf.bounce + 1) & 1];
+    const uint32_t qs = wf.slot_stride;
     const uint32_t p1 = cn->cls[1], p2 = p1 + cn->cls[2], p3 = p2 + cn->cls[3], total = p3 + cn->cls[0];
     if (q == 0 && threadIdx.x == 0) nx->queued = p3;
     const uint32_t lo = (uint32_t)(((uint64_t)total * q) / per), hi = (uint32_t)(((uint64_t)total * (q + 1)) / per);
@@ -350,7 +368,8 @@ __global__ void __launch_bounds__(kShadeBlock) wf_shade(const KernelParams kp, c
         const uint32_t k = i < p1 ? 1u : (i < p2 ? 2u : (i < p3 ? 3u : 0u));
         const uint32_t start = k == 1u ? 0u : (k == 2u ? p1 : (k == 3u ? p2 : p3));
         const uint32_t slot = wf.cls_list[(size_t)k * wf.slot_stride + seg0 + (i - start)];
-        const float4 o4 = qr[4u * slot], d4 = qr[4u * slot + 1u], h = qr[4u * slot + 2u], ps = qr[4u * slot + 3u];
+        const size_t js = seg0 + slot;
+        const float4 o4 = qb[qf(js, 0, qs)], d4 = qb[qf(js, 1, qs)], h = qb[qf(js, 2, qs)], ps = qb[qf(js, 3, qs)];
         const uint32_t pid = __float_as_uint(o4.w);
         const uint32_t depth = __float_as_uint(d4.w);
         const int32_t htri = __float_as_int(h.w);
@@ -375,24 +394,23 @@ __global__ void __launch_bounds__(kShadeBlock) wf_shade(const KernelParams kp, c
         } else {
             V3 color = xyz(ps);
             uint32_t sd = __float_as_uint(ps.w);
-            float4* nr = qr2 + 4u * i;                       // whole 64-B record written
+            const size_t ji = seg0 + i;                     // the whole next record is written
             if (qe && (int32_t)depth >= kp.max_depth && !qe_roulette(sd, color)) {
                 // killed by the roulette: zero radiance, an empty slot in queue b+1
                 wf.radiance[pid] = make_float4(0, 0, 0, 0);
-                nr[0] = pack(v3(0, 0, 0), pid);
-                nr[1] = pack(v3(0, 0, 0), kNoRay);
-                nr[2] = make_float4(0, 0, 0, 0);
-                nr[3] = make_float4(0, 0, 0, 0);
+                qb2[qf(ji, 0, qs)] = pack(v3(0, 0, 0), pid);
+                qb2[qf(ji, 1, qs)] = pack(v3(0, 0, 0), kNoRay);
+                qb2[qf(ji, 2, qs)] = make_float4(0, 0, 0, 0);
+                qb2[qf(ji, 3, qs)] = make_float4(0, 0, 0, 0);
             } else {
                 c.shades++;
                 const GpuGeom& gm = geoms[__float_as_uint(tris[htri + 1].w)];
                 V3 o = xyz(o4), d = xyz(d4);
                 if (qe) scatter<true>(gm, sc.normals, htri, h.y, h.z, h.x, 0, sd, color, o, d);
                 else scatter<false>(gm, sc.normals, htri, h.y, h.z, h.x, kp.fresnel_kd, sd, color, o, d);
-                nr[0] = pack(o, pid);
-                nr[1] = pack(d, depth + 1u);
-                nr[2] = make_float4(0, 0, 0, 0);
-                nr[3] = pack(color, sd);
+                qb2[qf(ji, 0, qs)] = pack(o, pid);
+                qb2[qf(ji, 1, qs)] = pack(d, depth + 1u);
+                qb2[qf(ji, 3, qs)] = pack(color, sd);
                 c.rays++;
             }
         }
