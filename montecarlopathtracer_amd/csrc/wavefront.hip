@@ -66,6 +66,14 @@ __device__ __forceinline__ float4 pack(V3 v, uint32_t w) { return make_float4(v.
 #ifndef MCPT_WF_SOA
 #define MCPT_WF_SOA 1
 #endif
+// Material sort (1): extend appends each finished slot to its segment's class
+// list and shade gathers the records list by list (one material per wave).
+// Slot order (0, default): shade reads its segment's queue in slot order --
+// dense streams, no class lists, the merged samplers absorb the material mix --
+// and appends continuing rays to the next queue with one LDS atomic per wave.
+#ifndef MCPT_WF_SORT
+#define MCPT_WF_SORT 0
+#endif
 __device__ __forceinline__ size_t qf(uint32_t slot, uint32_t k, uint32_t stride) {
 #if MCPT_WF_SOA
     return (size_t)k * stride + slot;
@@ -294,10 +302,14 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
             // CV: scatter while depth < max_depth (CUTracer.cu:103-160); QE: while
             // bounce < 3*depth (rtx.hlsl:312), roulette is drawn in shade
             const int32_t lim = kp.mode == kModeQE ? 3 * kp.max_depth : kp.max_depth;
+#if MCPT_WF_SORT
             if (r.htri >= 0 && depth != kNoRay && (int32_t)depth < lim) {
                 const GpuGeom& gm = geoms[__float_as_uint(tris[r.htri + 1].w)];
                 if (!is_emitter(gm)) cls = material_class(gm);
             }
+#else
+            (void)lim;
+#endif
             if (nslot < count) {
                 slot = nslot;
                 start(no4, nd4);
@@ -306,9 +318,13 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
             }
             qb[qf(seg0 + fslot, 2, qs)] = hrec;
         }
+#if MCPT_WF_SORT
 #pragma unroll
         for (uint32_t k = 0; k < 4; k++)
             out[k].append(cls == k, fslot, lcnt + k, wf.cls_list + (size_t)k * wf.slot_stride + seg0);
+#else
+        (void)cls;
+#endif
         // ---- prefetch the next ray of every lane that just started one -------
         const bool want = fin && mode != kDead;
         const uint32_t ns = cur_chunk.take(want, lcnt + 4);
@@ -319,8 +335,10 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
         WF_STAMP(tm_hand);
         if (!__ballot(mode != kDead)) break;
     }
+#if MCPT_WF_SORT
 #pragma unroll
     for (uint32_t k = 0; k < 4; k++) out[k].flush(lcnt + k, wf.cls_list + (size_t)k * wf.slot_stride + seg0);
+#endif
 #ifdef MCPT_PHASE_TIMING
     if ((threadIdx.x & 63u) == 0) {
         atomicAdd(kp.stats + 8, tm_setup);
@@ -416,6 +434,95 @@ __global__ void __launch_bounds__(kShadeBlock) wf_shade(const KernelParams kp, c
         }
     }
     flush_counters(c, kp.stats);
+}
+
+// ---- shade in slot order (MCPT_WF_SORT 0): one workgroup per segment --------
+// Reads the segment's queue b as dense streams (o, d, hit, throughput/rng),
+// finishes terminated paths (radiance by path id) and scatters the others; a
+// continuing ray goes to the next free slot of the segment's queue b+1 (one
+// LDS atomic per wave, 64 consecutive slots), so queue b+1 is dense.  Queue
+// order is scheduling-dependent, but nothing reads it (state keyed by pid).
+template <int BLOCK>
+__global__ void __launch_bounds__(BLOCK) wf_shade_slots(const KernelParams kp, const WfParams wf) {
+    const uint32_t g = blockIdx.x;
+    if (g >= wf.nseg) return;
+    __shared__ uint32_t lnext;
+    const WfCounters* cn = wf.cnt + (size_t)wf.bounce * wf.nseg + g;
+    WfCounters* nx = wf.cnt + (size_t)(wf.bounce + 1) * wf.nseg + g;
+    const uint32_t total = cn->queued;
+    if (threadIdx.x == 0) lnext = 0;
+    __syncthreads();
+    const GpuScene& sc = kp.scene;
+    const float4* tris = reinterpret_cast<const float4*>(sc.image + sc.off_tris);
+    const GpuGeom* geoms = reinterpret_cast<const GpuGeom*>(sc.image + sc.off_geoms);
+    const size_t seg0 = (size_t)g * wf.seg;
+    const float4* qb = wf.q[wf.bounce & 1];
+    float4* qb2 = wf.q[(wf.bounce + 1) & 1];
+    const uint32_t qs = wf.slot_stride;
+    const bool qe = kp.mode == kModeQE;
+    const int lane = (int)(threadIdx.x & 63u);
+    Counters c = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (uint32_t base = 0; base < total; base += BLOCK) {      // block-uniform trip count
+        const uint32_t i = base + threadIdx.x;
+        bool cont = false;
+        uint32_t pid = 0, depth = kNoRay, sd = 0;
+        V3 o = v3(0, 0, 0), d = v3(0, 0, 0), color = v3(0, 0, 0);
+        if (i < total) {
+            const size_t js = seg0 + i;
+            const float4 o4 = qb[qf(js, 0, qs)], d4 = qb[qf(js, 1, qs)], h = qb[qf(js, 2, qs)], ps = qb[qf(js, 3, qs)];
+            pid = __float_as_uint(o4.w);
+            depth = __float_as_uint(d4.w);
+            const int32_t htri = __float_as_int(h.w);
+            color = xyz(ps);
+            sd = __float_as_uint(ps.w);
+            // CV: miss -> 0; emitter -> color*Ka*ILLUM (:111-113); terminal query
+            // (:162-175); else scatter.  QE: miss / bounce >= 3*depth -> 0; roulette
+            // from bounce `depth` on; emitter -> color*Ka (rtx.hlsl:312-331)
+            V3 L = v3(0, 0, 0);
+            bool term = true;
+            if (htri >= 0 && depth != kNoRay) {
+                const GpuGeom& gm = geoms[__float_as_uint(tris[htri + 1].w)];
+                if (qe) {
+                    if ((int32_t)depth < 3 * kp.max_depth &&
+                        ((int32_t)depth < kp.max_depth || qe_roulette(sd, color))) {
+                        if (is_emitter(gm)) L = emitted(color, gm, 1.0f);
+                        else term = false;
+                    }
+                } else if ((int32_t)depth >= kp.max_depth || is_emitter(gm)) {
+                    L = emitted(color, gm, kp.illum);
+                } else {
+                    term = false;
+                }
+                if (!term) {
+                    c.shades++;
+                    o = xyz(o4);
+                    d = xyz(d4);
+                    if (qe) scatter<true>(gm, sc.normals, htri, h.y, h.z, h.x, 0, sd, color, o, d);
+                    else scatter<false>(gm, sc.normals, htri, h.y, h.z, h.x, kp.fresnel_kd, sd, color, o, d);
+                    cont = true;
+                    c.rays++;
+                }
+            }
+            if (term) wf.radiance[pid] = make_float4(L.x, L.y, L.z, 0.0f);   // (kNoRay slots: 0)
+        }
+        // next ray: the wave's continuing lanes take consecutive slots of queue b+1
+        const uint64_t m = __ballot(cont);
+        if (m) {
+            const int leader = __ffsll((unsigned long long)m) - 1;
+            uint32_t b0 = 0;
+            if (lane == leader) b0 = atomicAdd(&lnext, (uint32_t)__popcll(m));
+            b0 = __shfl(b0, leader);
+            if (cont) {
+                const size_t ji = seg0 + b0 + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                qb2[qf(ji, 0, qs)] = pack(o, pid);
+                qb2[qf(ji, 1, qs)] = pack(d, depth + 1u);
+                qb2[qf(ji, 3, qs)] = pack(color, sd);
+            }
+        }
+    }
+    flush_counters(c, kp.stats);
+    __syncthreads();
+    if (threadIdx.x == 0) nx->queued = lnext;
 }
 
 // ---- accumulate: samples of the batch in sample order -> partial sums -------
@@ -514,7 +621,15 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams& wf_in, in
                     e = launch_extend<false, 8, kGlobalBlock>(kp, wf, (int)nseg, (size_t)8 * kGlobalBlock * 16 + 32,
                                                               st);
                 if (e != hipSuccess) return e;
+#if MCPT_WF_SORT
                 hipLaunchKernelGGL(wf_shade, dim3(nseg * per), dim3(kShadeBlock), 0, st, kp, wf, per);
+#else
+                (void)per;
+                if (in_lds)
+                    hipLaunchKernelGGL(wf_shade_slots<1024>, dim3(nseg), dim3(1024), 0, st, kp, wf);
+                else
+                    hipLaunchKernelGGL(wf_shade_slots<256>, dim3(nseg), dim3(256), 0, st, kp, wf);
+#endif
                 if ((e = hipGetLastError()) != hipSuccess) return e;
             }
             hipLaunchKernelGGL(wf_accumulate, dim3((wf.nb + 255u) / 256u, ncb), dim3(256), 0, st, kp, wf);
