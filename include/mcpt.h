@@ -94,6 +94,10 @@ typedef struct {
                                    rays identical; ~1-2% faster).  The counts are deterministic:
                                    a counting render of the same params reports what a lean one
                                    did.  0 (default): count everything */
+    int32_t wf_sort;            /* wavefront: 1 = material sort (extend files each finished ray in
+                                   its material's list, shade runs one material per wave over
+                                   the lists); 0 (default) = shade in queue order (dense reads,
+                                   faster); same image */
 } mcpt_render_params;
 
 enum {

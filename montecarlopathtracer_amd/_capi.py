@@ -55,6 +55,7 @@ class RenderParamsC(C.Structure):
         ("seed", C.c_uint64), ("prev_count", C.c_uint32), ("fresnel_kd", C.c_int32),
         ("tile", C.c_int32), ("shard_count", C.c_int32), ("shard_index", C.c_int32), ("packed", C.c_int32),
         ("pipeline", C.c_int32), ("wf_batch", C.c_uint32), ("mode", C.c_int32), ("lean", C.c_int32),
+        ("wf_sort", C.c_int32),
     ]
 
 

@@ -351,6 +351,7 @@ struct Plan {
     size_t out_pixels;
     int pipeline;
     uint32_t wf_capacity;        // paths per wavefront batch
+    int32_t wf_sort;             // wavefront material sort (mcpt_render_params::wf_sort)
 };
 
 Plan make_plan(const mcpt_scene& s, const mcpt_render_params* p) {
@@ -434,6 +435,7 @@ Plan make_plan(const mcpt_scene& s, const mcpt_render_params* p) {
     if (p->pipeline != MCPT_PIPELINE_MEGAKERNEL && p->pipeline != MCPT_PIPELINE_WAVEFRONT)
         throw mcpt::Error{MCPT_E_INVALID, "unknown pipeline"};
     pl.pipeline = p->pipeline;
+    pl.wf_sort = p->wf_sort ? 1 : 0;
     {
         // default batch: big (160 B of queues per path; fewer launches, shorter
         // relative tails).  C2 2^24 5.59, 2^25 6.43, 2^26 7.07, 2^27 7.31, 2^28 7.24;
@@ -513,6 +515,7 @@ mcpt::WfParams prepare_wavefront(mcpt_scene& s, const Plan& pl) {
     const char* e = std::getenv("MCPT_WF_REFILL");
     const int th = e ? std::atoi(e) : 16;
     w.refill_thresh = th < 1 ? 1 : (th > 64 ? 64 : th);
+    w.sort = pl.wf_sort;
     return w;
 }
 

@@ -168,6 +168,7 @@ struct WfParams {
     uint32_t group_shift;                // paths are dealt to segments in groups of 2^group_shift
     int32_t bounce;
     int32_t refill_thresh;               // idle lanes before an extend wave refills
+    int32_t sort;                        // 1: material sort (class lists), 0: shade in queue order
 };
 
 size_t lds_bytes_in_lds(uint32_t image_bytes, int S);

@@ -66,14 +66,13 @@ __device__ __forceinline__ float4 pack(V3 v, uint32_t w) { return make_float4(v.
 #ifndef MCPT_WF_SOA
 #define MCPT_WF_SOA 1
 #endif
-// Material sort (1): extend appends each finished slot to its segment's class
-// list and shade gathers the records list by list (one material per wave).
-// Slot order (0, default): shade reads its segment's queue in slot order --
-// dense streams, no class lists, the merged samplers absorb the material mix --
-// and appends continuing rays to the next queue with one LDS atomic per wave.
-#ifndef MCPT_WF_SORT
-#define MCPT_WF_SORT 0
-#endif
+// WfParams::sort (mcpt_render_params::wf_sort) -- material sort (1): extend
+// appends each finished slot to its segment's class list and shade gathers
+// the records list by list (one material per wave).  Queue order (0, default):
+// shade reads its segment's queue in slot order -- dense streams, no class
+// lists, the merged samplers absorb the material mix -- and appends continuing
+// rays to the next queue with one LDS atomic per wave (C2 wavefront 7.56 ->
+// 10.03 G rays/s: the sorted shade's gathers cost more than the divergence).
 __device__ __forceinline__ size_t qf(uint32_t slot, uint32_t k, uint32_t stride) {
 #if MCPT_WF_SOA
     return (size_t)k * stride + slot;
@@ -302,14 +301,10 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
             // CV: scatter while depth < max_depth (CUTracer.cu:103-160); QE: while
             // bounce < 3*depth (rtx.hlsl:312), roulette is drawn in shade
             const int32_t lim = kp.mode == kModeQE ? 3 * kp.max_depth : kp.max_depth;
-#if MCPT_WF_SORT
-            if (r.htri >= 0 && depth != kNoRay && (int32_t)depth < lim) {
+            if (wf.sort && r.htri >= 0 && depth != kNoRay && (int32_t)depth < lim) {
                 const GpuGeom& gm = geoms[__float_as_uint(tris[r.htri + 1].w)];
                 if (!is_emitter(gm)) cls = material_class(gm);
             }
-#else
-            (void)lim;
-#endif
             if (nslot < count) {
                 slot = nslot;
                 start(no4, nd4);
@@ -318,13 +313,11 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
             }
             qb[qf(seg0 + fslot, 2, qs)] = hrec;
         }
-#if MCPT_WF_SORT
+        if (wf.sort) {
 #pragma unroll
-        for (uint32_t k = 0; k < 4; k++)
-            out[k].append(cls == k, fslot, lcnt + k, wf.cls_list + (size_t)k * wf.slot_stride + seg0);
-#else
-        (void)cls;
-#endif
+            for (uint32_t k = 0; k < 4; k++)
+                out[k].append(cls == k, fslot, lcnt + k, wf.cls_list + (size_t)k * wf.slot_stride + seg0);
+        }
         // ---- prefetch the next ray of every lane that just started one -------
         const bool want = fin && mode != kDead;
         const uint32_t ns = cur_chunk.take(want, lcnt + 4);
@@ -335,10 +328,10 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
         WF_STAMP(tm_hand);
         if (!__ballot(mode != kDead)) break;
     }
-#if MCPT_WF_SORT
+    if (wf.sort) {
 #pragma unroll
-    for (uint32_t k = 0; k < 4; k++) out[k].flush(lcnt + k, wf.cls_list + (size_t)k * wf.slot_stride + seg0);
-#endif
+        for (uint32_t k = 0; k < 4; k++) out[k].flush(lcnt + k, wf.cls_list + (size_t)k * wf.slot_stride + seg0);
+    }
 #ifdef MCPT_PHASE_TIMING
     if ((threadIdx.x & 63u) == 0) {
         atomicAdd(kp.stats + 8, tm_setup);
@@ -436,7 +429,7 @@ __global__ void __launch_bounds__(kShadeBlock) wf_shade(const KernelParams kp, c
     flush_counters(c, kp.stats);
 }
 
-// ---- shade in slot order (MCPT_WF_SORT 0): one workgroup per segment --------
+// ---- shade in queue order (wf_sort 0): one workgroup per segment -----------
 // Reads the segment's queue b as dense streams (o, d, hit, throughput/rng),
 // finishes terminated paths (radiance by path id) and scatters the others; a
 // continuing ray goes to the next free slot of the segment's queue b+1 (one
@@ -621,15 +614,12 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams& wf_in, in
                     e = launch_extend<false, 8, kGlobalBlock>(kp, wf, (int)nseg, (size_t)8 * kGlobalBlock * 16 + 32,
                                                               st);
                 if (e != hipSuccess) return e;
-#if MCPT_WF_SORT
-                hipLaunchKernelGGL(wf_shade, dim3(nseg * per), dim3(kShadeBlock), 0, st, kp, wf, per);
-#else
-                (void)per;
-                if (in_lds)
+                if (wf.sort)
+                    hipLaunchKernelGGL(wf_shade, dim3(nseg * per), dim3(kShadeBlock), 0, st, kp, wf, per);
+                else if (in_lds)
                     hipLaunchKernelGGL(wf_shade_slots<1024>, dim3(nseg), dim3(1024), 0, st, kp, wf);
                 else
                     hipLaunchKernelGGL(wf_shade_slots<256>, dim3(nseg), dim3(256), 0, st, kp, wf);
-#endif
                 if ((e = hipGetLastError()) != hipSuccess) return e;
             }
             hipLaunchKernelGGL(wf_accumulate, dim3((wf.nb + 255u) / 256u, ncb), dim3(256), 0, st, kp, wf);

@@ -173,6 +173,7 @@ class RenderParams:
     wf_batch: int = 0                 # wavefront paths in flight per batch, 0 = 2^27 (2^28 global scenes)
     mode: str = "cvmctracer"          # or "quinengine": rtx.hlsl path semantics (see for_quinengine)
     lean: bool = False                # megakernel without traversal counters (same image; bench timing)
+    wf_sort: bool = False             # wavefront: material-sorted shade (class lists); same image
 
     @staticmethod
     def for_scene(scene_id: int, **kw) -> "RenderParams":
@@ -211,6 +212,7 @@ class RenderParams:
             raise ValueError(f"mode must be one of {sorted(MODES)}")
         p.mode = MODES[self.mode]
         p.lean = 1 if self.lean else 0
+        p.wf_sort = 1 if self.wf_sort else 0
         return p
 
     def output_pixels(self) -> int:

@@ -8,7 +8,7 @@ statistical pin against the reference's own 1000-spp render.
   single-GPU image bit for bit; a second render is bit-identical (determinism);
   the image is finite and the light is the brightest region.
 * the same frame through the wavefront pipeline: bit-identical image, equal
-  counters.
+  counters; and C5 (4096 spp) likewise, twice (determinism).
 * RenderScene's progressive loop (10 launches x 100 spp, prevCount running
   mean, CUTracer.cu:378-398) at 800x600 with the published-render variant
   (luminance 30, untinted Fresnel) matches CV/result1.png statistically.
@@ -94,6 +94,29 @@ def test_fullsize_pipelines_agree(mcpt, scene01):
     assert torch.equal(img[:, :3], ref[:, :3])
     for k in ("rays", "paths", "inner_visits", "leaf_visits", "tri_tests", "shades"):
         assert st[k] == rs[k], (k, st[k], rs[k])
+
+
+def test_c5_wavefront_equals_megakernel_and_is_deterministic(mcpt, scene01):
+    """C5 (1024x1024 @ 4096 spp, BASELINE configs[4]) on one GPU: the wavefront
+    pipeline (its batches span several 32-sample chunks) renders the
+    megakernel's frame bit for bit with equal counters, and twice the same."""
+    import torch
+    W = H = 1024
+    stream = torch.cuda.current_stream().cuda_stream
+    out = {}
+    for name, pipeline in (("mega", "megakernel"), ("wave", "wavefront"), ("wave2", "wavefront")):
+        p = mcpt.RenderParams(width=W, height=H, spp=4096, spp_chunk=32, pipeline=pipeline)
+        fb = torch.zeros((H * W, 4), dtype=torch.float32, device="cuda")
+        scene01.render_device(p, fb.data_ptr(), stream)
+        torch.cuda.synchronize()
+        out[name] = (fb, scene01.stats())
+    ref, rs = out["mega"]
+    assert rs["rays"] > 1.3e10
+    for name in ("wave", "wave2"):
+        img, st = out[name]
+        assert torch.equal(img[:, :3], ref[:, :3]), name
+        for k in ("rays", "paths", "inner_visits", "leaf_visits", "tri_tests", "shades"):
+            assert st[k] == rs[k], (name, k, st[k], rs[k])
 
 
 def test_progressive_render_matches_reference_image(mcpt):

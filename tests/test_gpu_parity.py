@@ -39,7 +39,7 @@ def _oracle_render(oracle_mod, scene_path, W, H, spp, chunk, depth, seed, fkd, i
     return o.render(p, out)
 
 
-@pytest.mark.parametrize("pipeline", ["megakernel", "wavefront"])
+@pytest.mark.parametrize("pipeline", ["megakernel", "wavefront", "wavefront-sorted"])
 @pytest.mark.parametrize("case", CASES, ids=[f"{c[0]}-{c[1]}x{c[2]}-spp{c[3]}-d{c[5]}" for c in CASES])
 def test_image_and_counters_match_oracle(mcpt, oracle_mod, case, pipeline):
     sc, W, H, spp, chunk, depth, seed, fkd, illum = case
@@ -49,7 +49,9 @@ def test_image_and_counters_match_oracle(mcpt, oracle_mod, case, pipeline):
                              node_boxes=_node_boxes(mcpt, path))
     scene = mcpt.Scene(mcpt.ObjModel(path))
     p = mcpt.RenderParams.for_scene(scene_id, width=W, height=H, spp=spp, spp_chunk=chunk, max_depth=depth,
-                                    seed=seed, fresnel_kd=bool(fkd), illum=illum, pipeline=pipeline)
+                                    seed=seed, fresnel_kd=bool(fkd), illum=illum,
+                                    pipeline="wavefront" if pipeline.startswith("wavefront") else pipeline,
+                                    wf_sort=pipeline == "wavefront-sorted")
     img, st = scene.render(p)
     assert st["variant"] in ((1, 2, 3) if pipeline == "megakernel" else (4, 5))
     rmse = float(np.sqrt(np.mean((img - ref) ** 2)))
