@@ -159,7 +159,7 @@ def _qe_params(mcpt, W, H, spp, chunk, depth, seed, **kw):
                                             seed=seed, **kw)
 
 
-@pytest.mark.parametrize("pipeline", ["megakernel", "wavefront"])
+@pytest.mark.parametrize("pipeline", ["megakernel", "wavefront", "wavefront-sorted"])
 @pytest.mark.parametrize("case", QE_CASES, ids=[f"qe-{c[0]}-{c[1]}x{c[2]}-d{c[5]}" for c in QE_CASES])
 def test_quinengine_mode_matches_oracle(mcpt, oracle_mod, case, pipeline):
     """rtx.hlsl semantics (roulette, 3x depth cap, no ILLUM, gamma accumulation, QE camera)."""
@@ -170,7 +170,9 @@ def test_quinengine_mode_matches_oracle(mcpt, oracle_mod, case, pipeline):
                                                seed=seed, illum=1.0, fov=45.0, fresnel_kd=0, threads=8,
                                                mode=oracle_mod.MODE_QE, node_boxes=_node_boxes(mcpt, path)))
     scene = mcpt.Scene(mcpt.ObjModel(path))
-    img, st = scene.render(_qe_params(mcpt, W, H, spp, chunk, depth, seed, pipeline=pipeline))
+    img, st = scene.render(_qe_params(mcpt, W, H, spp, chunk, depth, seed,
+                                      pipeline="wavefront" if pipeline.startswith("wavefront") else pipeline,
+                                      wf_sort=pipeline == "wavefront-sorted"))
     assert np.array_equal(img, ref), f"max abs diff {np.abs(img - ref).max()}"
     for k in ("rays", "paths", "inner_visits", "leaf_visits", "leaf_refs", "tri_tests", "shades"):
         assert st[k] == rc[k], (k, st[k], rc[k])
