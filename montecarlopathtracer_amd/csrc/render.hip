@@ -63,16 +63,20 @@ __global__ void __launch_bounds__(BLOCK, (!IN_LDS && COUNT) ? 4 : 1) path_kernel
     const uint2* nodes;
     const uint32_t* leafs;
     const GpuGeom* geoms;
+    // LDS: [traversal stack S x BLOCK x 16 B | scene image].  The stack at LDS
+    // address 0 makes a slot address (sp & (S-1)) << log2(BLOCK*16) | tid * 16:
+    // fewer instructions per push and pop than an offset base
+    unsigned char* const lds_image = smem + (size_t)S * BLOCK * 16;
     if constexpr (IN_LDS) {
         const uint4* src = reinterpret_cast<const uint4*>(sc.image);
-        uint4* dst = reinterpret_cast<uint4*>(smem);
+        uint4* dst = reinterpret_cast<uint4*>(lds_image);
         const uint32_t n16 = sc.image_bytes / 16u;
         for (uint32_t i = (uint32_t)tid; i < n16; i += BLOCK) dst[i] = src[i];
         __syncthreads();
-        tris = reinterpret_cast<const float4*>(smem + sc.off_tris);
-        nodes = reinterpret_cast<const uint2*>(smem + sc.off_nodes) + 1;   // node i at slot i+1
-        leafs = reinterpret_cast<const uint32_t*>(smem + sc.off_leafs);
-        geoms = reinterpret_cast<const GpuGeom*>(smem + sc.off_geoms);
+        tris = reinterpret_cast<const float4*>(lds_image + sc.off_tris);
+        nodes = reinterpret_cast<const uint2*>(lds_image + sc.off_nodes) + 1;   // node i at slot i+1
+        leafs = reinterpret_cast<const uint32_t*>(lds_image + sc.off_leafs);
+        geoms = reinterpret_cast<const GpuGeom*>(lds_image + sc.off_geoms);
     } else {
         tris = reinterpret_cast<const float4*>(sc.image + sc.off_tris);
         nodes = reinterpret_cast<const uint2*>(sc.image + sc.off_nodes) + 1;
@@ -80,7 +84,7 @@ __global__ void __launch_bounds__(BLOCK, (!IN_LDS && COUNT) ? 4 : 1) path_kernel
         geoms = reinterpret_cast<const GpuGeom*>(sc.image + sc.off_geoms);
     }
     const uint4* pairs = reinterpret_cast<const uint4*>(sc.image + sc.off_nodes);   // 48-B pair records (global variant)
-    uint4* st = reinterpret_cast<uint4*>(smem + kp.lds_stack_off) + tid;   // [S][BLOCK] x 16 B
+    uint4* st = reinterpret_cast<uint4*>(smem) + tid;   // [S][BLOCK] x 16 B
     const uint32_t gl = blockIdx.x * BLOCK + (uint32_t)tid;
     uint4* spill = kp.spill + gl;
     const uint32_t spill_stride = kp.total_lanes;
@@ -439,7 +443,6 @@ hipError_t launch_render(const KernelParams& kp_in, int cus, hipStream_t st, hip
                          hipEvent_t ev2, float4* fb, int* variant_out) {
     KernelParams kp = kp_in;
     const uint32_t img = kp.scene.image_bytes;
-    kp.lds_stack_off = (!kp.scene.node_boxes && lds_bytes_in_lds(img, 4) <= kMaxLds) ? img : 0u;
     kp.total_lanes = (uint32_t)total_lanes_for(img, cus);
     hipError_t e = hipMemsetAsync(kp.counter, 0, sizeof(uint32_t), st);
     if (e != hipSuccess) return e;

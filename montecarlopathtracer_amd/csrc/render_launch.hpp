@@ -91,7 +91,6 @@ struct KernelParams {
     unsigned long long* stats;           // 8 counters
     uint4* spill;                        // traversal-stack spill [32][total_lanes]
     uint32_t total_lanes;
-    uint32_t lds_stack_off;              // LDS offset of the stack arrays
     uint32_t* unit_counters;             // optional [total_units][4]: rays, inner, leaf, tests
     int32_t ready_thresh;                // lanes ready before a shading round (1..64)
     int32_t lean;                        // 1: no per-step traversal counters (mcpt_render_params::lean)

@@ -56,6 +56,33 @@ __device__ __forceinline__ float sel3(int a, float x, float y, float z) {
     return a == 0 ? x : (a == 1 ? y : z);
 }
 
+// Stack slot (i mod S) of this lane, st + (i & (S-1)) * stride, as one
+// v_lshl_add_u32 on the LDS address after the mask (LLVM canonicalises the
+// index to (i << k) & mask and then needs a shift, an and and an add: one
+// instruction more on every push and pop).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) u32x4 lds_uint4;
+__device__ __forceinline__ uint4 ld4(const lds_uint4* p) {
+    const u32x4 v = *p;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void st4(lds_uint4* p, uint4 v) { *p = u32x4{v.x, v.y, v.z, v.w}; }
+#ifndef MCPT_SLOT_ASM
+#define MCPT_SLOT_ASM 1
+#endif
+template <int S>
+__device__ __forceinline__ lds_uint4* slot_of(uint4* st, int stride, int32_t i) {
+#if MCPT_SLOT_ASM
+    const uint32_t base = (uint32_t)(size_t)(lds_uint4*)st;
+    const uint32_t shift = 31u - (uint32_t)__builtin_clz((uint32_t)stride * 16u);
+    uint32_t a;
+    asm("v_lshl_add_u32 %0, %1, %2, %3" : "=v"(a) : "v"((uint32_t)i & (uint32_t)(S - 1)), "s"(shift), "v"(base));
+    return (lds_uint4*)(size_t)a;
+#else
+    return (lds_uint4*)(st + (i & (S - 1)) * stride);
+#endif
+}
+
 // lane modes of the persistent loop
 constexpr int kDead = 0;    // no more work
 constexpr int kTrav = 1;    // traversing its current ray
@@ -282,12 +309,14 @@ __device__ __forceinline__ bool pop_entry(RayState& r, uint4* st, int stride, ui
             e = spill[(uint32_t)r.sp * spill_stride];
             r.lo = r.sp;
         } else {
-            e = top ? *top : st[(r.sp & (S - 1)) * stride];
+            if (top) e = *top;
+            else e = ld4(slot_of<S>(st, stride, r.sp));
         }
     } else {                                  // refill the freed slot with the next older entry
-        uint4* slot = st + (r.sp & (S - 1)) * stride;
-        e = top ? *top : *slot;
-        if (r.sp >= S) *slot = spill[(uint32_t)(r.sp - S) * spill_stride];
+        lds_uint4* slot = slot_of<S>(st, stride, r.sp);
+        if (top) e = *top;
+        else e = ld4(slot);
+        if (r.sp >= S) st4(slot, spill[(uint32_t)(r.sp - S) * spill_stride]);
     }
     r.nw0 = e.x;
     r.nw1 = e.y;
@@ -357,18 +386,18 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
                 // pp ? tmin : max(t, tmin) without the select: a pp lane's t is
                 // (+0) * (+-inf) = NaN (da = +-0, oa == sv), and max returns tmin
                 const float plo = max_qnan(t, r.tmin);
-                uint4* slot = st + (r.sp & (S - 1)) * stride;
+                lds_uint4* slot = slot_of<S>(st, stride, r.sp);
                 if constexpr (!BOXES) {
                     if (r.sp - r.lo == S) {           // LDS part full: its oldest entry (same slot) to memory
-                        spill[(uint32_t)r.lo * spill_stride] = *slot;
+                        spill[(uint32_t)r.lo * spill_stride] = ld4(slot);
                         r.lo++;
                         if constexpr (COUNT) c.spills++;
                     }
                 } else if (r.sp >= S) {
-                    spill[(uint32_t)(r.sp - S) * spill_stride] = *slot;
+                    spill[(uint32_t)(r.sp - S) * spill_stride] = ld4(slot);
                     if constexpr (COUNT) c.spills++;
                 }
-                *slot = make_uint4(f0, f1, __float_as_uint(plo), __float_as_uint(r.tmax));
+                st4(slot, make_uint4(f0, f1, __float_as_uint(plo), __float_as_uint(r.tmax)));
                 r.sp++;
                 if constexpr (!BOXES)                // here push_it & !pp == both; te = NaN for pp
                     r.tmax = min_qnan(te, r.tmax);
@@ -393,7 +422,7 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
     // the stack's top slot, read ahead: the pop after this leaf's last tests
     // then needs no LDS round trip of its own (unused if the leaf goes on or
     // the stack is empty -- the slot index is in range either way)
-    const uint4 top = st[((r.sp - 1) & (S - 1)) * stride];
+    const uint4 top = ld4(slot_of<S>(st, stride, r.sp - 1));
     if (r.lpos < r.lend) {
         // both triangles' records are read before either test runs, so the two
         // LDS round trips (leaf ref -> triangle) overlap instead of chaining; a

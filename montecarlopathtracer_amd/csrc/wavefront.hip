@@ -198,8 +198,9 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
     }
     const int tid = (int)threadIdx.x;
     const GpuScene& sc = kp.scene;
-    // LDS: [scene image | stack S x BLOCK x 16 B | 5 counters]
-    uint32_t* lcnt = reinterpret_cast<uint32_t*>(smem + kp.lds_stack_off + (size_t)S * BLOCK * 16);
+    // LDS: [stack S x BLOCK x 16 B | scene image (IN_LDS) | 5 counters]
+    unsigned char* const lds_image = smem + (size_t)S * BLOCK * 16;
+    uint32_t* lcnt = reinterpret_cast<uint32_t*>(lds_image + (IN_LDS ? sc.image_bytes : 0u));
     if (tid < 5) lcnt[tid] = 0;
     const float4* tris;
     const uint2* nodes;
@@ -207,13 +208,13 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
     const GpuGeom* geoms;
     if constexpr (IN_LDS) {
         const uint4* src = reinterpret_cast<const uint4*>(sc.image);
-        uint4* dst = reinterpret_cast<uint4*>(smem);
+        uint4* dst = reinterpret_cast<uint4*>(lds_image);
         const uint32_t n16 = sc.image_bytes / 16u;
         for (uint32_t i = (uint32_t)tid; i < n16; i += BLOCK) dst[i] = src[i];
-        tris = reinterpret_cast<const float4*>(smem + sc.off_tris);
-        nodes = reinterpret_cast<const uint2*>(smem + sc.off_nodes) + 1;
-        leafs = reinterpret_cast<const uint32_t*>(smem + sc.off_leafs);
-        geoms = reinterpret_cast<const GpuGeom*>(smem + sc.off_geoms);
+        tris = reinterpret_cast<const float4*>(lds_image + sc.off_tris);
+        nodes = reinterpret_cast<const uint2*>(lds_image + sc.off_nodes) + 1;
+        leafs = reinterpret_cast<const uint32_t*>(lds_image + sc.off_leafs);
+        geoms = reinterpret_cast<const GpuGeom*>(lds_image + sc.off_geoms);
     } else {
         tris = reinterpret_cast<const float4*>(sc.image + sc.off_tris);
         nodes = reinterpret_cast<const uint2*>(sc.image + sc.off_nodes) + 1;
@@ -222,7 +223,7 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
     }
     const uint4* pairs = reinterpret_cast<const uint4*>(sc.image + sc.off_nodes);   // 48-B pair records (global variant)
     __syncthreads();
-    uint4* st = reinterpret_cast<uint4*>(smem + kp.lds_stack_off) + tid;
+    uint4* st = reinterpret_cast<uint4*>(smem) + tid;
     uint4* spill = kp.spill + (blockIdx.x * BLOCK + (uint32_t)tid);
     const uint32_t spill_stride = kp.total_lanes;
     const size_t seg0 = (size_t)g * wf.seg;
@@ -571,7 +572,6 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams& wf_in, in
     KernelParams kp = kp_in;
     const uint32_t img = kp.scene.image_bytes;
     const bool in_lds = wf_in_lds(img);
-    kp.lds_stack_off = in_lds ? img : 0u;
     kp.total_lanes = (uint32_t)total_lanes_for(img, cus);
     const uint32_t nseg = (uint32_t)wavefront_segments(img, cus);
     const uint32_t per = in_lds ? 4u : 1u;                         // shade workgroups per segment
