@@ -56,10 +56,9 @@ __device__ __forceinline__ float sel3(int a, float x, float y, float z) {
     return a == 0 ? x : (a == 1 ? y : z);
 }
 
-// Stack slot (i mod S) of this lane, st + (i & (S-1)) * stride, as one
-// v_lshl_add_u32 on the LDS address after the mask (LLVM canonicalises the
-// index to (i << k) & mask and then needs a shift, an and and an add: one
-// instruction more on every push and pop).
+// Stack slot (i mod S) of this lane.  RayState::sp and ::lo count stack
+// entries in units of one slot row (stride x 16 B), so the slot address is the
+// masked position OR the lane's base -- one instruction on every push and pop.
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) u32x4 lds_uint4;
 __device__ __forceinline__ uint4 ld4(const lds_uint4* p) {
@@ -67,20 +66,14 @@ __device__ __forceinline__ uint4 ld4(const lds_uint4* p) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 __device__ __forceinline__ void st4(lds_uint4* p, uint4 v) { *p = u32x4{v.x, v.y, v.z, v.w}; }
-#ifndef MCPT_SLOT_ASM
-#define MCPT_SLOT_ASM 1
-#endif
 template <int S>
-__device__ __forceinline__ lds_uint4* slot_of(uint4* st, int stride, int32_t i) {
-#if MCPT_SLOT_ASM
+__device__ __forceinline__ lds_uint4* slot_of(uint4* st, int stride, int32_t pos) {
+    // pos = stack index x (stride x 16 B), so the slot's byte offset is pos's
+    // bits under the mask, OR'd with this lane's base (the stack starts at LDS
+    // address 0 and a lane's base is below one slot row): one v_and_or_b32
     const uint32_t base = (uint32_t)(size_t)(lds_uint4*)st;
-    const uint32_t shift = 31u - (uint32_t)__builtin_clz((uint32_t)stride * 16u);
-    uint32_t a;
-    asm("v_lshl_add_u32 %0, %1, %2, %3" : "=v"(a) : "v"((uint32_t)i & (uint32_t)(S - 1)), "s"(shift), "v"(base));
-    return (lds_uint4*)(size_t)a;
-#else
-    return (lds_uint4*)(st + (i & (S - 1)) * stride);
-#endif
+    const uint32_t row = (uint32_t)stride * 16u;
+    return (lds_uint4*)(size_t)(((uint32_t)pos & ((uint32_t)(S - 1) * row)) | base);
 }
 
 // lane modes of the persistent loop
@@ -99,7 +92,7 @@ struct RayState {
     float tmax;                          // the interval's far end times kEpsHi (rounded), see begin_ray
     float best;
     uint32_t nw0, nw1, bprio;            // current node record
-    int32_t sp, htri;
+    int32_t sp, htri;                    // sp, lo: stack positions x (slot row bytes), see slot_of
     int32_t lo;                          // stack entries [0, lo) live in the spill memory
     uint32_t lpos, lend;                 // leaf refs still to test (capped leaf loop)
     float hbeta, hgamma;
@@ -301,12 +294,13 @@ __device__ __forceinline__ bool box_hit(const RayState& r, uint32_t b0, uint32_t
 template <int S, bool LAZY>
 __device__ __forceinline__ bool pop_entry(RayState& r, uint4* st, int stride, uint4* __restrict__ spill,
                                           uint32_t spill_stride, const uint4* top = nullptr) {
+    const int32_t U = stride * 16;          // one stack position
     if (r.sp == 0) return false;
-    r.sp--;
+    r.sp -= U;
     uint4 e;
     if constexpr (LAZY) {
         if (r.sp < r.lo) {                    // LDS part empty: the entry is in memory
-            e = spill[(uint32_t)r.sp * spill_stride];
+            e = spill[((uint32_t)r.sp / (uint32_t)U) * spill_stride];
             r.lo = r.sp;
         } else {
             if (top) e = *top;
@@ -316,7 +310,7 @@ __device__ __forceinline__ bool pop_entry(RayState& r, uint4* st, int stride, ui
         lds_uint4* slot = slot_of<S>(st, stride, r.sp);
         if (top) e = *top;
         else e = ld4(slot);
-        if (r.sp >= S) st4(slot, spill[(uint32_t)(r.sp - S) * spill_stride]);
+        if (r.sp >= S * U) st4(slot, spill[((uint32_t)r.sp / (uint32_t)U - S) * spill_stride]);
     }
     r.nw0 = e.x;
     r.nw1 = e.y;
@@ -331,6 +325,7 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
                                           const uint2* __restrict__ nodes1, const uint32_t* __restrict__ leafs,
                                           uint4* st, int stride, uint4* __restrict__ spill, uint32_t spill_stride,
                                           Counters& c MCPT_LU_PARAM, const uint4* __restrict__ pairs = nullptr) {
+    const int32_t U = stride * 16;            // one stack position (see slot_of)
     if (r.lpos == r.lend) {                   // between leaves: descend
         // the walk advances r.nw0/r.nw1 in place (local copies written back at
         // the cap cost register moves on every path through the loop)
@@ -388,17 +383,17 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
                 const float plo = max_qnan(t, r.tmin);
                 lds_uint4* slot = slot_of<S>(st, stride, r.sp);
                 if constexpr (!BOXES) {
-                    if (r.sp - r.lo == S) {           // LDS part full: its oldest entry (same slot) to memory
-                        spill[(uint32_t)r.lo * spill_stride] = ld4(slot);
-                        r.lo++;
+                    if (r.sp - r.lo == S * U) {       // LDS part full: its oldest entry (same slot) to memory
+                        spill[((uint32_t)r.lo / (uint32_t)U) * spill_stride] = ld4(slot);
+                        r.lo += U;
                         if constexpr (COUNT) c.spills++;
                     }
-                } else if (r.sp >= S) {
-                    spill[(uint32_t)(r.sp - S) * spill_stride] = ld4(slot);
+                } else if (r.sp >= S * U) {
+                    spill[((uint32_t)r.sp / (uint32_t)U - S) * spill_stride] = ld4(slot);
                     if constexpr (COUNT) c.spills++;
                 }
                 st4(slot, make_uint4(f0, f1, __float_as_uint(plo), __float_as_uint(r.tmax)));
-                r.sp++;
+                r.sp += U;
                 if constexpr (!BOXES)                // here push_it & !pp == both; te = NaN for pp
                     r.tmax = min_qnan(te, r.tmax);
             }
@@ -422,7 +417,7 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
     // the stack's top slot, read ahead: the pop after this leaf's last tests
     // then needs no LDS round trip of its own (unused if the leaf goes on or
     // the stack is empty -- the slot index is in range either way)
-    const uint4 top = ld4(slot_of<S>(st, stride, r.sp - 1));
+    const uint4 top = ld4(slot_of<S>(st, stride, r.sp - U));
     if (r.lpos < r.lend) {
         // both triangles' records are read before either test runs, so the two
         // LDS round trips (leaf ref -> triangle) overlap instead of chaining; a
