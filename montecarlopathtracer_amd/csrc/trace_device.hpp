@@ -319,6 +319,105 @@ __device__ __forceinline__ bool pop_entry(RayState& r, uint4* st, int stride, ui
     return !(r.best <= r.tmin * kEpsLo);
 }
 
+// Descent of a ray between leaves: at most `cap` inner-node steps (the node
+// record and interval stay in the ray state); 0 = cap reached mid-descent,
+// 1 = a leaf reached (its refs in [lpos, lend)), 2 = the walk ended (a
+// global-memory scene's box cull popped past the last interval).
+// COUNT = false (lean renders): the counters are compiled out.
+template <int S, bool BOXES = false, bool COUNT = true>
+__device__ __forceinline__ int descend_steps(RayState& r, const uint2* __restrict__ nodes1, uint4* st, int stride,
+                                             uint4* __restrict__ spill, uint32_t spill_stride, Counters& c,
+                                             const uint4* __restrict__ pairs, int cap MCPT_LU_PARAM) {
+    const int32_t U = stride * 16;            // one stack position (see slot_of)
+    // the walk advances r.nw0/r.nw1 in place (local copies written back at
+    // the cap cost register moves on every path through the loop)
+    uint32_t& w0 = r.nw0;
+    uint32_t& w1 = r.nw1;
+    int steps = 0;
+    while ((w0 >> 30) != 3u) {
+        if (steps == cap) return 0;           // resume next call
+        steps++;
+        if constexpr (COUNT) c.inner++;
+        MCPT_LANE_USE(desc_w, desc_l, lu);
+        const uint32_t left = w0 & 0x3FFFFFFFu;
+        uint4 pr, bx0, bx1;
+        if constexpr (BOXES) {            // 48-B pair record: words, box(left), box(right)
+            const uint4* rec = pairs + 3u * ((left - 1u) >> 1);
+            pr = rec[0];
+            bx0 = rec[1];
+            bx1 = rec[2];
+        } else {
+            pr = *reinterpret_cast<const uint4*>(nodes1 + left);   // children left, left+1
+        }
+        const int a = (int)(w0 >> 30);
+        const float sv = __uint_as_float(w1);
+        const float oa = sel3(a, r.o.x, r.o.y, r.o.z);
+        const float ia = sel3(a, r.ix, r.iy, r.iz);
+        const float t = (sv - oa) * ia;
+        // near side: below the plane, or on it and heading down; pp = ray inside
+        // the plane (both children).  Only an origin exactly on the plane needs
+        // the direction, so its select and tests sit in a rarely taken branch.
+        bool below = oa < sv, pp = false;
+        if (__builtin_expect(oa == sv, 0)) {
+            const float da = sel3(a, r.d.x, r.d.y, r.d.z);
+            below = da <= 0.0f;
+            pp = da == 0.0f;
+        }
+        // if/else chain of the oracle, evaluated branch-free
+        const float te = t * kEpsHi;
+        const bool no = !(t > 0.0f) | (t > r.tmax);                 // near child only
+        const bool fo = te < r.tmin;                                // far child only
+        const bool go_far = !pp & !no & fo;
+        const bool both = !pp & !no & !fo;                          // push far, go near
+        bool push_it = pp | both;
+        bool near_ok = true, far_ok = true;
+        if constexpr (BOXES) {
+            const bool hl = box_hit(r, bx0.x, bx0.y, bx0.z);
+            const bool hr = box_hit(r, bx0.w, bx1.x, bx1.y);
+            near_ok = below ? hl : hr;
+            far_ok = below ? hr : hl;
+            push_it = push_it & far_ok;
+        }
+        const uint32_t f0 = below ? pr.z : pr.x, f1 = below ? pr.w : pr.y;     // far child record
+        if (push_it) {
+            // pp ? tmin : max(t, tmin) without the select: a pp lane's t is
+            // (+0) * (+-inf) = NaN (da = +-0, oa == sv), and max returns tmin
+            const float plo = max_qnan(t, r.tmin);
+            lds_uint4* slot = slot_of<S>(st, stride, r.sp);
+            if constexpr (!BOXES) {
+                if (r.sp - r.lo == S * U) {       // LDS part full: its oldest entry (same slot) to memory
+                    spill[((uint32_t)r.lo / (uint32_t)U) * spill_stride] = ld4(slot);
+                    r.lo += U;
+                    if constexpr (COUNT) c.spills++;
+                }
+            } else if (r.sp >= S * U) {
+                spill[((uint32_t)r.sp / (uint32_t)U - S) * spill_stride] = ld4(slot);
+                if constexpr (COUNT) c.spills++;
+            }
+            st4(slot, make_uint4(f0, f1, __float_as_uint(plo), __float_as_uint(r.tmax)));
+            r.sp += U;
+            if constexpr (!BOXES)                // here push_it & !pp == both; te = NaN for pp
+                r.tmax = min_qnan(te, r.tmax);
+        }
+        if constexpr (BOXES)                                        // the near child's interval,
+            if (both) r.tmax = te < r.tmax ? te : r.tmax;           // pushed far or not
+        // the child entered: the near one, or the far one when go_far (the
+        // left record when below != go_far) -- two selects, not four
+        const bool enter_left = below != go_far;
+        w0 = enter_left ? pr.x : pr.z;
+        w1 = enter_left ? pr.y : pr.w;
+        if constexpr (BOXES) {
+            if (!(go_far ? far_ok : near_ok)) {   // the chosen child's box is missed: next interval
+                if (!pop_entry<S, !BOXES>(r, st, stride, spill, spill_stride)) return 2;
+            }
+        }
+    }
+    if constexpr (COUNT) c.leaf++;
+    r.lpos = w0 & 0x3FFFFFFFu;
+    r.lend = r.lpos + w1;
+    return 1;
+}
+
 // COUNT = false (lean renders): the counters below are compiled out (rays stay)
 template <int S, bool BOXES = false, bool COUNT = true>
 __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict__ tris,
@@ -327,92 +426,10 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
                                           Counters& c MCPT_LU_PARAM, const uint4* __restrict__ pairs = nullptr) {
     const int32_t U = stride * 16;            // one stack position (see slot_of)
     if (r.lpos == r.lend) {                   // between leaves: descend
-        // the walk advances r.nw0/r.nw1 in place (local copies written back at
-        // the cap cost register moves on every path through the loop)
-        uint32_t& w0 = r.nw0;
-        uint32_t& w1 = r.nw1;
-        int steps = 0;
-        while ((w0 >> 30) != 3u) {
-            if (steps == (BOXES ? MCPT_DESCENT_CAP_GLOBAL : MCPT_DESCENT_CAP)) return false;   // resume next call
-            steps++;
-            if constexpr (COUNT) c.inner++;
-            MCPT_LANE_USE(desc_w, desc_l, lu);
-            const uint32_t left = w0 & 0x3FFFFFFFu;
-            uint4 pr, bx0, bx1;
-            if constexpr (BOXES) {            // 48-B pair record: words, box(left), box(right)
-                const uint4* rec = pairs + 3u * ((left - 1u) >> 1);
-                pr = rec[0];
-                bx0 = rec[1];
-                bx1 = rec[2];
-            } else {
-                pr = *reinterpret_cast<const uint4*>(nodes1 + left);   // children left, left+1
-            }
-            const int a = (int)(w0 >> 30);
-            const float sv = __uint_as_float(w1);
-            const float oa = sel3(a, r.o.x, r.o.y, r.o.z);
-            const float ia = sel3(a, r.ix, r.iy, r.iz);
-            const float t = (sv - oa) * ia;
-            // near side: below the plane, or on it and heading down; pp = ray inside
-            // the plane (both children).  Only an origin exactly on the plane needs
-            // the direction, so its select and tests sit in a rarely taken branch.
-            bool below = oa < sv, pp = false;
-            if (__builtin_expect(oa == sv, 0)) {
-                const float da = sel3(a, r.d.x, r.d.y, r.d.z);
-                below = da <= 0.0f;
-                pp = da == 0.0f;
-            }
-            // if/else chain of the oracle, evaluated branch-free
-            const float te = t * kEpsHi;
-            const bool no = !(t > 0.0f) | (t > r.tmax);                 // near child only
-            const bool fo = te < r.tmin;                                // far child only
-            const bool go_far = !pp & !no & fo;
-            const bool both = !pp & !no & !fo;                          // push far, go near
-            bool push_it = pp | both;
-            bool near_ok = true, far_ok = true;
-            if constexpr (BOXES) {
-                const bool hl = box_hit(r, bx0.x, bx0.y, bx0.z);
-                const bool hr = box_hit(r, bx0.w, bx1.x, bx1.y);
-                near_ok = below ? hl : hr;
-                far_ok = below ? hr : hl;
-                push_it = push_it & far_ok;
-            }
-            const uint32_t f0 = below ? pr.z : pr.x, f1 = below ? pr.w : pr.y;     // far child record
-            if (push_it) {
-                // pp ? tmin : max(t, tmin) without the select: a pp lane's t is
-                // (+0) * (+-inf) = NaN (da = +-0, oa == sv), and max returns tmin
-                const float plo = max_qnan(t, r.tmin);
-                lds_uint4* slot = slot_of<S>(st, stride, r.sp);
-                if constexpr (!BOXES) {
-                    if (r.sp - r.lo == S * U) {       // LDS part full: its oldest entry (same slot) to memory
-                        spill[((uint32_t)r.lo / (uint32_t)U) * spill_stride] = ld4(slot);
-                        r.lo += U;
-                        if constexpr (COUNT) c.spills++;
-                    }
-                } else if (r.sp >= S * U) {
-                    spill[((uint32_t)r.sp / (uint32_t)U - S) * spill_stride] = ld4(slot);
-                    if constexpr (COUNT) c.spills++;
-                }
-                st4(slot, make_uint4(f0, f1, __float_as_uint(plo), __float_as_uint(r.tmax)));
-                r.sp += U;
-                if constexpr (!BOXES)                // here push_it & !pp == both; te = NaN for pp
-                    r.tmax = min_qnan(te, r.tmax);
-            }
-            if constexpr (BOXES)                                        // the near child's interval,
-                if (both) r.tmax = te < r.tmax ? te : r.tmax;           // pushed far or not
-            // the child entered: the near one, or the far one when go_far (the
-            // left record when below != go_far) -- two selects, not four
-            const bool enter_left = below != go_far;
-            w0 = enter_left ? pr.x : pr.z;
-            w1 = enter_left ? pr.y : pr.w;
-            if constexpr (BOXES) {
-                if (!(go_far ? far_ok : near_ok)) {   // the chosen child's box is missed: next interval
-                    if (!pop_entry<S, !BOXES>(r, st, stride, spill, spill_stride)) return true;
-                }
-            }
-        }
-        if constexpr (COUNT) c.leaf++;
-        r.lpos = w0 & 0x3FFFFFFFu;
-        r.lend = r.lpos + w1;
+        const int k = descend_steps<S, BOXES, COUNT>(r, nodes1, st, stride, spill, spill_stride, c, pairs,
+                                                      BOXES ? MCPT_DESCENT_CAP_GLOBAL : MCPT_DESCENT_CAP MCPT_LU_ARG);
+        if (k == 0) return false;
+        if (k == 2) return true;
     }
     // the stack's top slot, read ahead: the pop after this leaf's last tests
     // then needs no LDS round trip of its own (unused if the leaf goes on or
