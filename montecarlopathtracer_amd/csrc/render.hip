@@ -40,7 +40,9 @@ namespace {
 // Both layouts run 16 waves per CU and need <= 128 VGPRs; keep an eye on the
 // global variant (at 130 it lost a quarter of its occupancy: C4 -20%).  An
 // explicit min-waves bound (__launch_bounds__(BLOCK, 4)) made it slower (C4
-// 1.81 vs 1.97 G rays/s), so the budget is kept by the code instead.
+// 1.81 vs 1.97 G rays/s), so the budget is kept by the code instead.  Five
+// lean workgroups per CU (LDS fits 5 x 32 KB; bound 5 -> 96 VGPRs, no scratch)
+// lost 3.7% on C4 against four.
 // sum of a unit's samples -> partial[chunk][v], or one tail sample's radiance
 __device__ __forceinline__ void store_part(const KernelParams& kp, uint32_t id, V3 part) {
     const float4 val = make_float4(part.x, part.y, part.z, 0.0f);

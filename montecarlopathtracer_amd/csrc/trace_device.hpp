@@ -260,24 +260,31 @@ __device__ __forceinline__ void test_tri(RayState& r, const float4* __restrict__
 __device__ __forceinline__ float h2f(uint32_t bits16) {
     return (float)__builtin_bit_cast(_Float16, (unsigned short)bits16);
 }
-__device__ __forceinline__ void box_slab(float o, float d, float inv, float blo, float bhi, float& lo, float& hi,
-                                         bool& out) {
-    if (d == 0.0f) {
-        out = out | (o < blo) | (o > bhi);
-    } else {
-        const float t0 = (blo - o) * inv, t1 = (bhi - o) * inv;
-        const float a0 = t0 < t1 ? t0 : t1, a1 = t0 < t1 ? t1 : t0;
-        lo = a0 > lo ? a0 : lo;
-        hi = a1 < hi ? a1 : hi;
-    }
+// One slab of the box test for a nonzero direction component: the interval
+// update.  A zero component (the slab test degenerates to a containment test
+// of the origin) is handled by box_hit's rarely taken branch, so the six slabs
+// of a step's two boxes carry no per-slab branch and its exec-mask
+// bookkeeping (C4 +5.9%).
+__device__ __forceinline__ void box_slab(bool zero, float o, float inv, float blo, float bhi, float& lo, float& hi) {
+    const float t0 = (blo - o) * inv, t1 = (bhi - o) * inv;
+    const float a0 = t0 < t1 ? t0 : t1, a1 = t0 < t1 ? t1 : t0;
+    lo = (!zero & (a0 > lo)) ? a0 : lo;
+    hi = (!zero & (a1 < hi)) ? a1 : hi;
 }
 // box = lo.x lo.y | lo.z hi.x | hi.y hi.z as three packed fp16 pairs
 __device__ __forceinline__ bool box_hit(const RayState& r, uint32_t b0, uint32_t b1, uint32_t b2) {
     float lo = 0.0f, hi = r.best;
+    const bool zx = r.d.x == 0.0f, zy = r.d.y == 0.0f, zz = r.d.z == 0.0f;
+    const float lx = h2f(b0 & 0xFFFFu), hx = h2f(b1 >> 16);
+    const float ly = h2f(b0 >> 16), hy = h2f(b2 & 0xFFFFu);
+    const float lz = h2f(b1 & 0xFFFFu), hz = h2f(b2 >> 16);
+    box_slab(zx, r.o.x, r.ix, lx, hx, lo, hi);
+    box_slab(zy, r.o.y, r.iy, ly, hy, lo, hi);
+    box_slab(zz, r.o.z, r.iz, lz, hz, lo, hi);
     bool out = false;
-    box_slab(r.o.x, r.d.x, r.ix, h2f(b0 & 0xFFFFu), h2f(b1 >> 16), lo, hi, out);
-    box_slab(r.o.y, r.d.y, r.iy, h2f(b0 >> 16), h2f(b2 & 0xFFFFu), lo, hi, out);
-    box_slab(r.o.z, r.d.z, r.iz, h2f(b1 & 0xFFFFu), h2f(b2 >> 16), lo, hi, out);
+    if (__builtin_expect(zx | zy | zz, 0))   // a direction component is 0: the origin must lie in that slab
+        out = (zx & ((r.o.x < lx) | (r.o.x > hx))) | (zy & ((r.o.y < ly) | (r.o.y > hy))) |
+              (zz & ((r.o.z < lz) | (r.o.z > hz)));
     return !out && !(lo * kEpsLo > hi * kEpsHi);
 }
 
