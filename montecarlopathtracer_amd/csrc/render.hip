@@ -56,6 +56,7 @@ template <bool IN_LDS, int S, int BLOCK, bool DBG, bool QE, bool COUNT>
 // counting kernels of the global layout are held to 4 waves per SIMD (128 VGPRs)
 // by the launch bound; the lean (timed) kernels fit without it
 __global__ void __launch_bounds__(BLOCK, (!IN_LDS && COUNT) ? 4 : 1) path_kernel(const KernelParams kp) {
+    static_assert((BLOCK & (BLOCK - 1)) == 0, "stack slot addresses (slot_of) mask by a power-of-two block");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = (int)threadIdx.x;
     const int lane = tid & 63;
@@ -390,6 +391,7 @@ __global__ void __launch_bounds__(256) gather_kernel(const GatherParams g) {
 // so every lane reaches the wave-level counter flush.
 template <bool BOXES, int S>
 __global__ void __launch_bounds__(kQueryBlock) query_kernel(const QueryParams q) {
+    static_assert((kQueryBlock & (kQueryBlock - 1)) == 0, "stack slot addresses (slot_of) mask by a power-of-two block");
     __shared__ uint4 stk[S * kQueryBlock];
     const GpuScene& sc = q.scene;
     const int tid = (int)threadIdx.x;

@@ -188,6 +188,7 @@ struct ClassBuf {
 // ---- extend: closest hit of every ray of this workgroup's segment -----------
 template <bool IN_LDS, int S, int BLOCK>
 __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const WfParams wf) {
+    static_assert((BLOCK & (BLOCK - 1)) == 0, "stack slot addresses (slot_of) mask by a power-of-two block");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t g = blockIdx.x;
     WfCounters* cn = wf.cnt + (size_t)wf.bounce * wf.nseg + g;
