@@ -99,6 +99,28 @@ def live_counters(args) -> dict:
     return c
 
 
+def copy_bandwidth(dev, mib: int = 1024, reps: int = 10) -> dict:
+    """Stream-copy microbenchmark on this GPU (the measured copy
+    bandwidth is the roofline's second denominator): device-to-device copies
+    of a 1 GiB buffer, read + write bytes over HIP-event time."""
+    import torch
+    n = mib * (1 << 20) // 4
+    src = torch.ones(n, dtype=torch.float32, device=dev)
+    dst = torch.empty_like(src)
+    for _ in range(2):
+        dst.copy_(src)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        dst.copy_(src)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1)
+    gbs = 2.0 * n * 4 * reps / (ms * 1e-3) / 1e9
+    del src, dst
+    return {"GBps": round(gbs, 1), "method": f"torch copy_ of {mib} MiB x {reps}, (read + write) bytes / HIP-event time"}
+
+
 def cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -333,12 +355,21 @@ def main():
                                 "clock_GHz_under_pmc": round(cycles / (kern_ms * 1e6), 3),
                                 "formula": "SQ_INSTS_VALU / (CUs*4*cycles/2); lanes = SQ_THREAD_CYCLES_VALU / "
                                            "(64*SQ_ACTIVE_INST_VALU)"}
-        roof["binding_resource"] = ("VALU issue and lane divergence (the scene image is LDS-resident; HBM "
-                                    "carries only seeds, spills and the framebuffer)")
+        if world == 1:
+            cb = copy_bandwidth(dev)
+            if roof["achieved"] is not None and cb["GBps"] > 0:
+                cb["achieved_frac"] = round(roof["achieved"] / cb["GBps"], 5)
+            roof["peak_copy_measured"] = cb
+        in_lds = st["variant"] in (1, 2, 4)   # kernel variants that hold the scene image in LDS
+        roof["binding_resource"] = (("VALU issue and lane divergence (the scene image is LDS-resident; HBM "
+                                     "carries only seeds, spills and the framebuffer)") if in_lds else
+                                    ("memory latency of the node / triangle reads (scene image in global memory, "
+                                     "served by L1/L2/MALL; profiles/r02/c4_mem)"))
         roof["algorithmic"] = {"GBps": round(algo_gbs, 1), "bytes_per_ray": round(ab["survey"] / max(per_launch["rays"], 1), 1),
                                "bytes_per_launch": int(ab["survey"]),
                                "model": "SURVEY 8(d): 32*nodes+4*leafrefs+48*tris+96*shades+16*px",
-                               "served_from": "LDS (scene image) and L2 (normals), not HBM",
+                               "served_from": ("LDS (scene image) and L2 (normals), not HBM" if in_lds else
+                                               "L1 / L2 / MALL (scene image in global memory)"),
                                "own_layout_GBps": round(ab["own"] / (kern_ms * 1e-3) / 1e9, 1),
                                "per_ray": {k: round(per_launch[k] / max(per_launch["rays"], 1), 3) for k in
                                            ("inner_visits", "leaf_visits", "leaf_refs", "tri_tests", "shades")}}
