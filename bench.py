@@ -53,7 +53,31 @@ def _workload_args(args) -> list:
         (["--counting"] if args.counting else [])
 
 
-def pmc_pass(args, counters: list, tag: str, timeout_s: int = 150) -> dict:
+WF_KERNELS = (("wf_extend", "extend"), ("wf_shade", "shade"), ("wf_generate", "generate"),
+              ("wf_accumulate", "accumulate"))
+
+
+def read_wf_kernels(d: str) -> dict:
+    """Per wavefront kernel class, summed over its dispatches of one render:
+    counter values and the dispatches' durations (ns) from the PMC csv."""
+    import csv
+    import glob
+    out = {}
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                name = row.get("Kernel_Name", "")
+                cls = next((c for key, c in WF_KERNELS if key in name), None)
+                if cls is None:
+                    continue
+                k = out.setdefault(cls, {"ns": {}, "counters": {}})
+                k["ns"][row["Dispatch_Id"]] = int(row["End_Timestamp"]) - int(row["Start_Timestamp"])
+                cn = row["Counter_Name"]
+                k["counters"][cn] = k["counters"].get(cn, 0.0) + float(row["Counter_Value"])
+    return {c: {"ns": sum(v["ns"].values()), "dispatches": len(v["ns"]), **v["counters"]} for c, v in out.items()}
+
+
+def pmc_pass(args, counters: list, tag: str, timeout_s: int = 150, reader=None) -> dict:
     """One rocprofv3 PMC pass over ONE render of the same workload, in a child
     process (MI355X_MICROARCH.md 'rocprofv3 PMC slots': one pass per counter
     group -- FETCH_SIZE uses 3 of the 4 TCC slots, WRITE_SIZE 2).  Returns the
@@ -81,7 +105,7 @@ def pmc_pass(args, counters: list, tag: str, timeout_s: int = 150) -> dict:
         proc.wait()
         return {}
     try:
-        vals = read_counters(out) if proc.returncode == 0 else {}
+        vals = (reader or read_counters)(out) if proc.returncode == 0 else {}
     finally:
         shutil.rmtree(out, ignore_errors=True)
     return vals
@@ -97,6 +121,25 @@ def live_counters(args) -> dict:
                                     "SQ_WAVE_CYCLES", "GRBM_GUI_ACTIVE"])):
         c.update(pmc_pass(args, counters, tag))
     return c
+
+
+def wavefront_hbm(args) -> dict:
+    """Measured HBM bytes and time of each wavefront kernel over one render
+    (FETCH_SIZE doubled + WRITE_SIZE, as live_counters): the queue streams are
+    where this pipeline meets the HBM roofline."""
+    f = pmc_pass(args, ["FETCH_SIZE"], "wf_fetch", reader=read_wf_kernels)
+    w = pmc_pass(args, ["WRITE_SIZE"], "wf_write", reader=read_wf_kernels)
+    res = {}
+    for cls in f:
+        if cls not in w or "FETCH_SIZE" not in f[cls] or "WRITE_SIZE" not in w[cls]:
+            continue
+        rd = 2.0 * f[cls]["FETCH_SIZE"] * 1024.0
+        wr = w[cls]["WRITE_SIZE"] * 1024.0
+        ns = f[cls]["ns"]
+        res[cls] = {"hbm_read_GB": round(rd / 1e9, 3), "hbm_write_GB": round(wr / 1e9, 3), "ms": round(ns / 1e6, 3),
+                    "launches": f[cls]["dispatches"],
+                    "GBps": round((rd + wr) / max(ns, 1), 1), "frac": round((rd + wr) / max(ns, 1) / HBM_PEAK_GBS, 4)}
+    return res
 
 
 def copy_bandwidth(dev, mib: int = 1024, reps: int = 10) -> dict:
@@ -330,7 +373,16 @@ def main():
         roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
                 "traffic": None, "traffic_unit": "GB of HBM read+write per path-kernel launch",
                 "source": "rocprofv3 --pmc passes of this build and workload, run by this bench"}
-        if world == 1 and not args.no_pmc:
+        if world == 1 and not args.no_pmc and args.pipeline == "wavefront":
+            # per-kernel measured HBM traffic; `achieved` = the whole pipeline's bytes / its kernels' time
+            kh = wavefront_hbm(args)
+            if kh:
+                tot_b = sum((k["hbm_read_GB"] + k["hbm_write_GB"]) for k in kh.values())
+                tot_ms = sum(k["ms"] for k in kh.values())
+                gbs = tot_b / (tot_ms * 1e-3) if tot_ms > 0 else 0.0
+                roof.update(achieved=round(gbs, 2), frac=round(gbs / HBM_PEAK_GBS, 5), traffic=round(tot_b, 3),
+                            traffic_unit="GB of HBM read+write per frame (all wavefront kernels)", kernels=kh)
+        elif world == 1 and not args.no_pmc:
             # measured HBM bytes: FETCH_SIZE x2 (gfx950 streaming-read undercount) + WRITE_SIZE, KiB
             pmc = live_counters(args)
             if "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
@@ -360,6 +412,8 @@ def main():
             if roof["achieved"] is not None and cb["GBps"] > 0:
                 cb["achieved_frac"] = round(roof["achieved"] / cb["GBps"], 5)
             roof["peak_copy_measured"] = cb
+            for k in roof.get("kernels", {}).values():
+                k["frac_of_copy"] = round(k["GBps"] / cb["GBps"], 4) if cb["GBps"] > 0 else None
         in_lds = st["variant"] in (1, 2, 4)   # kernel variants that hold the scene image in LDS
         roof["binding_resource"] = (("VALU issue and lane divergence (the scene image is LDS-resident; HBM "
                                      "carries only seeds, spills and the framebuffer)") if in_lds else
