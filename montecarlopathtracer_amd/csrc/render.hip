@@ -296,7 +296,7 @@ __global__ void __launch_bounds__(BLOCK, (!IN_LDS && COUNT) ? 4 : 1) path_kernel
             }
             const uint64_t trv = __ballot(mode == kTrav);
             const uint64_t rdy = __ballot(mode == kReady);
-            if (!trv || __popcll(rdy) >= kp.ready_thresh) break;
+            if (!trv || (int)__popcll(rdy) >= kp.ready_thresh) break;
         }
         MCPT_STAMP(tm_trav);
     }
@@ -450,7 +450,7 @@ hipError_t launch_render(const KernelParams& kp_in, int cus, hipStream_t st, hip
     kp.total_lanes = (uint32_t)total_lanes_for(img, cus);
     hipError_t e = hipMemsetAsync(kp.counter, 0, sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
-    if (ev0) hipEventRecord(ev0, st);
+    if (ev0 && (e = hipEventRecord(ev0, st)) != hipSuccess) return e;
     int variant = 0;
     if (kp.scene.node_boxes) {                     // image built for global memory
         variant = 3;
@@ -466,9 +466,9 @@ hipError_t launch_render(const KernelParams& kp_in, int cus, hipStream_t st, hip
         e = launch_path<false, 8, kGlobalBlock>(kp, cus * kGlobalBlocksPerCu, (size_t)8 * kGlobalBlock * 16, st);
     }
     if (e != hipSuccess) return e;
-    if (ev1) hipEventRecord(ev1, st);
+    if (ev1 && (e = hipEventRecord(ev1, st)) != hipSuccess) return e;
     e = launch_reduce(kp, fb, st);
-    if (ev2) hipEventRecord(ev2, st);
+    if (e == hipSuccess && ev2) e = hipEventRecord(ev2, st);
     if (variant_out) *variant_out = variant;
     return e;
 }

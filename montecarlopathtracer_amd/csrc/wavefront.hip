@@ -283,7 +283,7 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
             }
             const uint64_t trv = __ballot(mode == kTrav);
             const uint64_t rdy = __ballot(mode == kReady);
-            if (!trv || __popcll(rdy) >= wf.refill_thresh) break;
+            if (!trv || (int)__popcll(rdy) >= wf.refill_thresh) break;
         }
         WF_STAMP(tm_trav);
         // ---- hand-off: hit record + per-material class list -----------------
@@ -577,7 +577,7 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams& wf_in, in
     const uint32_t nseg = (uint32_t)wavefront_segments(img, cus);
     const uint32_t per = in_lds ? 4u : 1u;                         // shade workgroups per segment
     hipError_t e = hipSuccess;
-    if (ev0) hipEventRecord(ev0, st);
+    if (ev0 && (e = hipEventRecord(ev0, st)) != hipSuccess) return e;
     for (uint32_t chunk = 0; chunk < kp.nchunks;) {
         WfParams wf = wf_in;
         wf.nseg = nseg;
@@ -627,9 +627,9 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams& wf_in, in
             if ((e = hipGetLastError()) != hipSuccess) return e;
         }
     }
-    if (ev1) hipEventRecord(ev1, st);
+    if (ev1 && (e = hipEventRecord(ev1, st)) != hipSuccess) return e;
     e = launch_reduce(kp, fb, st);
-    if (ev2) hipEventRecord(ev2, st);
+    if (e == hipSuccess && ev2) e = hipEventRecord(ev2, st);
     if (variant_out) *variant_out = in_lds ? 4 : 5;
     return e;
 }
