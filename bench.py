@@ -14,7 +14,10 @@ passes of this build and workload, run by this bench in child processes:
 FETCH_SIZE x2 + WRITE_SIZE) / its HIP-event duration; the kernel is bound by
 VALU issue, reported under roofline.valu (issue and lane fractions from the
 same passes); SURVEY.md section 8(d)'s algorithmic bytes (LDS/L2-served) are
-reported separately under roofline.algorithmic.  cpu_baseline = BASELINE
+reported separately under roofline.algorithmic.  Wavefront runs report each
+kernel's measured HBM traffic and rate under roofline.kernels (the queue
+streams: SURVEY 8(f)1), and every N = 1 run measures a 1 GiB device copy as
+the roofline's second denominator (roofline.peak_copy_measured).  cpu_baseline = BASELINE
 configs[0] (C1: 512x512, 16 spp, whole frame, one thread) on the CPU oracle,
 plus the same oracle on all of this process's cores over crops of the workload.
 

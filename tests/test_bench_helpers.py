@@ -1,0 +1,69 @@
+"""bench.py's host-side accounting (no GPU): SURVEY 8(d)'s bytes model and the
+rocprofv3 csv readers behind roofline.traffic / roofline.kernels, on small
+synthetic counter files in rocprofv3's csv layout."""
+import csv
+import importlib.util
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+HEADER = ["Correlation_Id", "Dispatch_Id", "Agent_Id", "Queue_Id", "Process_Id", "Thread_Id", "Grid_Size",
+          "Kernel_Id", "Kernel_Name", "Workgroup_Size", "LDS_Block_Size", "Scratch_Size", "VGPR_Count",
+          "Accum_VGPR_Count", "SGPR_Count", "Counter_Name", "Counter_Value", "Start_Timestamp", "End_Timestamp"]
+
+
+def _bench():
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def _write(d, rows):
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, "run_counter_collection.csv"), "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(HEADER)
+        for disp, name, cn, val, t0, t1 in rows:
+            w.writerow([disp, disp, "Agent 2", 1, 1, 1, 1024, 7, name, 256, 0, 0, 64, 0, 16, cn, val, t0, t1])
+
+
+def test_algorithmic_bytes_is_survey_formula():
+    b = _bench()
+    st = {"inner_visits": 10, "leaf_visits": 2, "leaf_refs": 3, "tri_tests": 3, "shades": 1}
+    ab = b.algorithmic_bytes(st, pixels=4)
+    assert ab["survey"] == 32 * 12 + 4 * 3 + 48 * 3 + 96 * 1 + 16 * 4
+    assert ab["own"] == 8 * 12 + 4 * 3 + 48 * 3 + 96 * 1 + 16 * 4
+
+
+def test_wavefront_kernel_reader_sums_dispatches(tmp_path):
+    b = _bench()
+    ext = "void mcpt::(anonymous namespace)::wf_extend<true, 4, 1024>(mcpt::KernelParams, mcpt::WfParams)"
+    shd = "void mcpt::(anonymous namespace)::wf_shade_slots<1024>(mcpt::KernelParams, mcpt::WfParams)"
+    other = "void at::native::vectorized_elementwise_kernel<4>(int)"
+    # counters summed over XCD rows of one dispatch, then over dispatches; time per dispatch once
+    _write(str(tmp_path / "p"), [
+        (1, ext, "FETCH_SIZE", 100.0, 1000, 3000), (1, ext, "FETCH_SIZE", 50.0, 1000, 3000),
+        (2, ext, "FETCH_SIZE", 10.0, 5000, 6000),
+        (3, shd, "FETCH_SIZE", 7.0, 7000, 7500),
+        (4, other, "FETCH_SIZE", 1e9, 0, 10),
+    ])
+    r = b.read_wf_kernels(str(tmp_path / "p"))
+    assert set(r) == {"extend", "shade"}
+    assert r["extend"]["FETCH_SIZE"] == 160.0 and r["extend"]["ns"] == 3000 and r["extend"]["dispatches"] == 2
+    assert r["shade"]["FETCH_SIZE"] == 7.0 and r["shade"]["ns"] == 500
+
+
+def test_path_kernel_reader_picks_the_lean_kernel(tmp_path):
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    from pmc_summary import read_counters
+    lean = "void mcpt::(anonymous namespace)::path_kernel<true, 4, 1024, false, false, false>(mcpt::KernelParams)"
+    counting = "void mcpt::(anonymous namespace)::path_kernel<true, 4, 1024, false, false, true>(mcpt::KernelParams)"
+    _write(str(tmp_path / "q"), [
+        (1, counting, "WRITE_SIZE", 999.0, 0, 1),
+        (2, lean, "WRITE_SIZE", 4.0, 0, 1), (2, lean, "WRITE_SIZE", 6.0, 0, 1),
+        (3, lean, "WRITE_SIZE", 20.0, 0, 1),
+    ])
+    # per-launch average over the lean kernel's dispatches: (10 + 20) / 2
+    assert read_counters(str(tmp_path / "q")) == {"WRITE_SIZE": 15.0}
