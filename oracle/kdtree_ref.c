@@ -115,7 +115,7 @@ void orc_kd_build(orc_scene* s) {
 
     bnode root;
     memset(&root, 0, sizeof root);
-    root.ids = malloc(sizeof(int) * (size_t)(n ? n : 1));
+    root.ids = malloc(sizeof(int) * (size_t)(n > 0 ? n : 1));
     root.nids = n;
     for (int i = 0; i < n; i++) root.ids[i] = i;
     root.box = node_aabb(&c, root.ids, n);

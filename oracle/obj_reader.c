@@ -132,7 +132,7 @@ static int find_add_group(orc_model* m, const char* name) {
 
 static void mat_init(orc_mat* mt, const char* name) {
     memset(mt, 0, sizeof *mt);
-    snprintf(mt->name, sizeof mt->name, "%s", name);
+    snprintf(mt->name, sizeof mt->name, "%.*s", (int)sizeof mt->name - 1, name);   /* long names truncated */
     mt->Ns = 1.0; mt->Tr = 0.0; mt->Ni = 1.0;   /* ObjReader.hpp:22 */
 }
 
