@@ -294,7 +294,7 @@ def main():
     if args.pmc_child:   # PMC pass: exactly one render of the timed kernel, then exit
         p = M.RenderParams.for_scene(scene_id, width=args.width, height=args.height, spp=args.spp,
                                      spp_chunk=args.spp_chunk, tile=8, pipeline=args.pipeline, wf_batch=args.wf_batch,
-                                     lean=args.pipeline == "megakernel" and not args.counting)
+                                     lean=not args.counting)
         fb = torch.zeros((p.output_pixels(), 4), dtype=torch.float32, device=dev)
         scene.render_device(p, fb.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
         torch.cuda.synchronize(dev)
@@ -302,7 +302,7 @@ def main():
     # timed renders run the megakernel lean (no per-step traversal counters, same
     # image and ray count); the node/leaf/triangle counts of the bytes model come
     # from one untimed counting render of the same frame (they are deterministic)
-    lean = args.pipeline == "megakernel" and not args.counting
+    lean = not args.counting
     p = M.RenderParams.for_scene(scene_id, width=args.width, height=args.height, spp=args.spp,
                                  spp_chunk=args.spp_chunk, tile=8, shard_count=world, shard_index=rank,
                                  packed=world > 1, pipeline=args.pipeline, wf_batch=args.wf_batch, lean=lean)
@@ -445,7 +445,8 @@ def main():
             "mpath_s": round(st["paths"] / elapsed / 1e6, 3),
             "rays_per_path": round(st["rays"] / max(st["paths"], 1), 4),
             "stack_spills_per_ray": round(st["stack_spills"] / max(st["rays"], 1), 4),
-            "timed_kernel": "lean megakernel (traversal counters compiled out)" if lean else "counting",
+            "timed_kernel": (f"lean {'megakernel' if args.pipeline == 'megakernel' else 'wavefront extend'} "
+                             "(traversal counters compiled out)") if lean else "counting",
             "counts_source": ("untimed counting render of the same frame; its rays equal the timed "
                               f"renders': {counts_match}") if lean else "timed renders",
             "kernel_ms_avg": round(kern_ms, 3),

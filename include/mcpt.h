@@ -91,7 +91,9 @@ typedef struct {
     int32_t mode;               /* MCPT_MODE_*: path semantics (default CVMCTracer)       */
     int32_t lean;               /* 1: the megakernel counts only rays (paths, shades, spills,
                                    inner/leaf visits, leaf refs, triangle tests read 0; image and
-                                   rays identical; ~1-2% faster).  The counts are deterministic:
+                                   rays identical; ~1-2% faster); the wavefront's extend drops
+                                   its traversal counters (spills, visits, refs, tests read 0;
+                                   rays, paths and shades stay).  The counts are deterministic:
                                    a counting render of the same params reports what a lean one
                                    did.  0 (default): count everything */
     int32_t wf_sort;            /* wavefront: 1 = material sort (extend files each finished ray in

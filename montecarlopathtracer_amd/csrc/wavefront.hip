@@ -186,7 +186,8 @@ struct ClassBuf {
 };
 
 // ---- extend: closest hit of every ray of this workgroup's segment -----------
-template <bool IN_LDS, int S, int BLOCK>
+// COUNT = false (lean renders): the traversal counters are compiled out
+template <bool IN_LDS, int S, int BLOCK, bool COUNT>
 __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const WfParams wf) {
     static_assert((BLOCK & (BLOCK - 1)) == 0, "stack slot addresses (slot_of) mask by a power-of-two block");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -279,7 +280,9 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
             }
 #endif
             if (mode == kTrav) {
-                if (trav_iter<S, !IN_LDS>(r, tris, nodes, leafs, st, BLOCK, spill, spill_stride, c MCPT_LU_ARG, pairs)) mode = kReady;
+                if (trav_iter<S, !IN_LDS, COUNT>(r, tris, nodes, leafs, st, BLOCK, spill, spill_stride, c MCPT_LU_ARG,
+                                                 pairs))
+                    mode = kReady;
             }
             const uint64_t trv = __ballot(mode == kTrav);
             const uint64_t rdy = __ballot(mode == kReady);
@@ -534,7 +537,7 @@ __global__ void __launch_bounds__(256) wf_accumulate(const KernelParams kp, cons
 
 template <bool IN_LDS, int S, int BLOCK>
 hipError_t launch_extend(const KernelParams& kp, const WfParams& wf, int grid, size_t lds, hipStream_t st) {
-    auto kern = wf_extend<IN_LDS, S, BLOCK>;
+    auto kern = kp.lean ? wf_extend<IN_LDS, S, BLOCK, false> : wf_extend<IN_LDS, S, BLOCK, true>;
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;

@@ -172,7 +172,7 @@ class RenderParams:
     pipeline: str = "megakernel"      # or "wavefront" (C5): identical image, different kernels
     wf_batch: int = 0                 # wavefront paths in flight per batch, 0 = 2^27 (2^28 global scenes)
     mode: str = "cvmctracer"          # or "quinengine": rtx.hlsl path semantics (see for_quinengine)
-    lean: bool = False                # megakernel without traversal counters (same image; bench timing)
+    lean: bool = False                # kernels without traversal counters (same image; bench timing)
     wf_sort: bool = False             # wavefront: material-sorted shade (class lists); same image
 
     @staticmethod

@@ -265,18 +265,23 @@ def test_ragged_chunks_with_tail_split_match_oracle(mcpt, oracle_mod, mode):
         assert st[k] == rc[k], (k, st[k], rc[k])
 
 
+@pytest.mark.parametrize("pipeline", ["megakernel", "wavefront"])
 @pytest.mark.parametrize("sc", ["scene01", "cornell_bunny70k"])
-def test_lean_megakernel_same_image(mcpt, sc):
-    """lean=True (the bench's timed kernel) compiles every counter but rays out:
-    same image and ray count as the counting kernel; the other counters read 0."""
+def test_lean_same_image(mcpt, sc, pipeline):
+    """lean=True (the bench's timed kernels) compiles the traversal counters
+    out: same image and ray count as the counting kernels; visits and tests
+    read 0 (the megakernel also drops shades; the wavefront's shade keeps them)."""
     path = mcpt.scene_path(sc)
     scene = mcpt.Scene(mcpt.ObjModel(path))
-    kw = dict(width=48, height=40, spp=6, spp_chunk=4, seed=9)
+    kw = dict(width=48, height=40, spp=6, spp_chunk=4, seed=9, pipeline=pipeline)
     img, st = scene.render(mcpt.RenderParams(**kw))
     img2, st2 = scene.render(mcpt.RenderParams(lean=True, **kw))
     assert np.array_equal(img, img2)
     assert st["rays"] == st2["rays"]
-    assert st["inner_visits"] > 0 and st2["inner_visits"] == 0 and st2["tri_tests"] == 0 and st2["shades"] == 0
+    if pipeline == "wavefront":
+        assert st["paths"] == st2["paths"]
+    assert st["inner_visits"] > 0 and st2["inner_visits"] == 0 and st2["tri_tests"] == 0
+    assert st2["shades"] == (0 if pipeline == "megakernel" else st["shades"])
 
 
 STRESS = [(sc, seed) for sc in ("scene01", "scene02", "scene03") for seed in (1, 0xBEEF, 0x4D435055)]
