@@ -512,8 +512,11 @@ mcpt::WfParams prepare_wavefront(mcpt_scene& s, const Plan& pl) {
     w.cnt = reinterpret_cast<mcpt::WfCounters*>(b);
     w.capacity = static_cast<uint32_t>(cap);       // paths per batch (pid range)
     w.slot_stride = static_cast<uint32_t>(cap_slots);
+    // idle lanes before an extend wave refills: 16 for scenes in LDS (C2 sweep
+    // 8 / 16 / 24: 10.08 / 10.28 / 10.19 G rays/s), 8 for scenes in global
+    // memory (C4 256 spp, 2..40: 6.18 / 6.20 (4-12) / 6.14 (16) / 5.79 (32) / 5.53)
     const char* e = std::getenv("MCPT_WF_REFILL");
-    const int th = e ? std::atoi(e) : 16;
+    const int th = e ? std::atoi(e) : (s.gpu.node_boxes ? 8 : 16);
     w.refill_thresh = th < 1 ? 1 : (th > 64 ? 64 : th);
     w.sort = pl.wf_sort;
     return w;
