@@ -123,6 +123,10 @@ struct mcpt_scene {
     hipEvent_t start = nullptr;         // primary: inputs ready on the caller's stream
     void* gather = nullptr;
     size_t gather_bytes = 0;
+    // wavefront: a second stream for every other batch, forked from and joined
+    // back into the caller's stream (created on first use)
+    hipStream_t wf_stream = nullptr;
+    hipEvent_t wf_fork = nullptr, wf_join = nullptr;
 
     ~mcpt_scene() {
         if (!on_device) return;
@@ -134,9 +138,10 @@ struct mcpt_scene {
             if (p) (void)hipFree(p);
         for (auto& t : pending) for (auto ev : t.e) (void)hipEventDestroy(ev);
         for (auto& t : free_timing) for (auto ev : t.e) (void)hipEventDestroy(ev);
-        for (hipEvent_t ev : {done, start})
+        for (hipEvent_t ev : {done, start, wf_fork, wf_join})
             if (ev) (void)hipEventDestroy(ev);
         if (stream) (void)hipStreamDestroy(stream);
+        if (wf_stream) (void)hipStreamDestroy(wf_stream);
         replicas.clear();                 // each replica frees on its own device
         if (prev >= 0) (void)hipSetDevice(prev);
     }
@@ -455,14 +460,15 @@ Plan make_plan(const mcpt_scene& s, const mcpt_render_params* p) {
 // ~3.5 ms) set the kernel's end: at 1024 spp, rank 0 of 8 ran 64.4 ms against
 // 55.5 ideal (86%); split 2 / 4 / 6 / 8 / 12 per lane: 92 / 96 / 98 / 97 / 96%,
 // 1-GPU frame unchanged (442 -> 440 ms at 6).
-void prepare_workspace(mcpt_scene& s, mcpt::KernelParams& k, bool tail_split = false) {
+void prepare_workspace(mcpt_scene& s, mcpt::KernelParams& k, bool tail_split = false, int spill_sets = 1) {
     ensure_buf(s.ws.partial, s.ws.partial_bytes, size_t(k.nchunks) * k.npix_local * 16);
     if (!s.ws.small) {
         HIP_TRY(hipMalloc(&s.ws.small, 256));
         HIP_TRY(hipMemset(s.ws.small, 0, 256));
     }
     const size_t lanes = static_cast<size_t>(mcpt::total_lanes_for(s.gpu.image_bytes, s.cus));
-    ensure_buf(s.ws.spill, s.ws.spill_bytes, 32 * lanes * 16);
+    // (the wavefront's two streams run extends concurrently: one spill area each)
+    ensure_buf(s.ws.spill, s.ws.spill_bytes, size_t(spill_sets) * 32 * lanes * 16);
     k.partial = static_cast<float4*>(s.ws.partial);
     k.counter = static_cast<uint32_t*>(s.ws.small);
     k.stats = reinterpret_cast<unsigned long long*>(static_cast<char*>(s.ws.small) + 64);
@@ -492,34 +498,42 @@ void prepare_workspace(mcpt_scene& s, mcpt::KernelParams& k, bool tail_split = f
 }
 
 // wavefront workspace: 2 ray queues (o, d float4), hits, 4 class lists,
-// path state and radiance, per-bounce counters -- carved from one buffer
-mcpt::WfParams prepare_wavefront(mcpt_scene& s, const Plan& pl) {
+// path state and radiance, per-bounce counters -- carved from one buffer, once
+// per stream (`sets`: batches alternate between two streams, each with its own)
+int wavefront_streams() {
+    // MCPT_WF_STREAMS=1: every batch on the caller's stream (A/B and tests)
+    const char* e = std::getenv("MCPT_WF_STREAMS");
+    return e && std::atoi(e) == 1 ? 1 : 2;
+}
+
+void prepare_wavefront(mcpt_scene& s, const Plan& pl, int sets, mcpt::WfParams* out) {
     const size_t cap = pl.wf_capacity;
     const size_t queries = pl.kp.mode == MCPT_MODE_QUINENGINE ? 3 * size_t(pl.kp.max_depth) + 1 : size_t(pl.kp.max_depth) + 1;
     const size_t bounces = (queries + 1) * size_t(mcpt::wavefront_segments(s.gpu.image_bytes, s.cus));
     // segments hold whole path groups (<= 2^14): up to nseg groups of slots beyond the paths
     const size_t cap_slots = cap + size_t(mcpt::wavefront_segments(s.gpu.image_bytes, s.cus)) * 16384;
     const size_t f4 = cap_slots * 16;
-    const size_t need = 2 * 4 * f4 + f4 + 4 * cap_slots * 4 + bounces * sizeof(mcpt::WfCounters) + 256;
-    ensure_buf(s.ws.wf, s.ws.wf_bytes, need);
-    char* b = static_cast<char*>(s.ws.wf);
-    mcpt::WfParams w;
-    std::memset(&w, 0, sizeof w);
-    w.q[0] = reinterpret_cast<float4*>(b); b += 4 * f4;
-    w.q[1] = reinterpret_cast<float4*>(b); b += 4 * f4;
-    w.radiance = reinterpret_cast<float4*>(b); b += f4;
-    w.cls_list = reinterpret_cast<uint32_t*>(b); b += 4 * cap_slots * 4;
-    w.cnt = reinterpret_cast<mcpt::WfCounters*>(b);
-    w.capacity = static_cast<uint32_t>(cap);       // paths per batch (pid range)
-    w.slot_stride = static_cast<uint32_t>(cap_slots);
+    const size_t need = (2 * 4 * f4 + f4 + 4 * cap_slots * 4 + bounces * sizeof(mcpt::WfCounters) + 256 + 255) & ~size_t(255);
+    ensure_buf(s.ws.wf, s.ws.wf_bytes, need * size_t(sets));
+    const char* e = std::getenv("MCPT_WF_REFILL");
     // idle lanes before an extend wave refills: 16 for scenes in LDS (C2 sweep
     // 8 / 16 / 24: 10.08 / 10.28 / 10.19 G rays/s), 8 for scenes in global
     // memory (C4 256 spp, 2..40: 6.18 / 6.20 (4-12) / 6.14 (16) / 5.79 (32) / 5.53)
-    const char* e = std::getenv("MCPT_WF_REFILL");
     const int th = e ? std::atoi(e) : (s.gpu.node_boxes ? 8 : 16);
-    w.refill_thresh = th < 1 ? 1 : (th > 64 ? 64 : th);
-    w.sort = pl.wf_sort;
-    return w;
+    for (int h = 0; h < sets; ++h) {
+        char* b = static_cast<char*>(s.ws.wf) + size_t(h) * need;
+        mcpt::WfParams& w = out[h];
+        std::memset(&w, 0, sizeof w);
+        w.q[0] = reinterpret_cast<float4*>(b); b += 4 * f4;
+        w.q[1] = reinterpret_cast<float4*>(b); b += 4 * f4;
+        w.radiance = reinterpret_cast<float4*>(b); b += f4;
+        w.cls_list = reinterpret_cast<uint32_t*>(b); b += 4 * cap_slots * 4;
+        w.cnt = reinterpret_cast<mcpt::WfCounters*>(b);
+        w.capacity = static_cast<uint32_t>(cap);       // paths per batch (pid range)
+        w.slot_stride = static_cast<uint32_t>(cap_slots);
+        w.refill_thresh = th < 1 ? 1 : (th > 64 ? 64 : th);
+        w.sort = pl.wf_sort;
+    }
 }
 
 void set_device(const mcpt_scene& s) {
@@ -546,7 +560,8 @@ void render_async(mcpt_scene& s, const mcpt_render_params* p, float* d_fb, hipSt
     Plan pl = make_plan(s, p);
     pl.kp.raw_mean = raw_mean ? 1 : 0;
     // the tail split hands units out by sample, so per-unit counters need whole units
-    prepare_workspace(s, pl.kp, pl.pipeline == MCPT_PIPELINE_MEGAKERNEL && !d_unit_counters);
+    const int wf_sets = pl.pipeline == MCPT_PIPELINE_WAVEFRONT ? wavefront_streams() : 1;
+    prepare_workspace(s, pl.kp, pl.pipeline == MCPT_PIPELINE_MEGAKERNEL && !d_unit_counters, wf_sets);
     pl.kp.unit_counters = d_unit_counters;
     Timing t;
     if (!s.free_timing.empty()) {
@@ -557,9 +572,16 @@ void render_async(mcpt_scene& s, const mcpt_render_params* p, float* d_fb, hipSt
     }
     if (pl.pipeline == MCPT_PIPELINE_WAVEFRONT) {
         if (d_unit_counters) throw mcpt::Error{MCPT_E_UNSUPPORTED, "unit counters need the megakernel pipeline"};
-        const mcpt::WfParams wf = prepare_wavefront(s, pl);
+        mcpt::WfParams wf[2];
+        prepare_wavefront(s, pl, wf_sets, wf);
+        if (wf_sets == 2 && !s.wf_stream) {
+            HIP_TRY(hipStreamCreateWithFlags(&s.wf_stream, hipStreamNonBlocking));
+            HIP_TRY(hipEventCreateWithFlags(&s.wf_fork, hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&s.wf_join, hipEventDisableTiming));
+        }
         const int queries = pl.kp.mode == MCPT_MODE_QUINENGINE ? 3 * pl.kp.max_depth + 1 : pl.kp.max_depth + 1;
-        HIP_TRY(mcpt::launch_wavefront(pl.kp, wf, s.cus, queries, st, t.e[0], t.e[1], t.e[2],
+        const mcpt::WfStreams ws2{wf_sets == 2 ? s.wf_stream : nullptr, s.wf_fork, s.wf_join};
+        HIP_TRY(mcpt::launch_wavefront(pl.kp, wf, wf_sets, ws2, s.cus, queries, st, t.e[0], t.e[1], t.e[2],
                                        reinterpret_cast<float4*>(d_fb), &s.last_variant));
     } else {
         HIP_TRY(mcpt::launch_render(pl.kp, s.cus, st, t.e[0], t.e[1], t.e[2], reinterpret_cast<float4*>(d_fb),
@@ -1115,8 +1137,12 @@ int mcpt_scene_reserve(mcpt_scene* s, const mcpt_render_params* p) {
         auto reserve = [&](mcpt_scene& sc, const mcpt_render_params* q) {
             set_device(sc);
             Plan pl = make_plan(sc, q);
-            prepare_workspace(sc, pl.kp, pl.pipeline == MCPT_PIPELINE_MEGAKERNEL);
-            if (pl.pipeline == MCPT_PIPELINE_WAVEFRONT) (void)prepare_wavefront(sc, pl);
+            const int sets = pl.pipeline == MCPT_PIPELINE_WAVEFRONT ? wavefront_streams() : 1;
+            prepare_workspace(sc, pl.kp, pl.pipeline == MCPT_PIPELINE_MEGAKERNEL, sets);
+            if (pl.pipeline == MCPT_PIPELINE_WAVEFRONT) {
+                mcpt::WfParams wf[2];
+                prepare_wavefront(sc, pl, sets, wf);
+            }
         };
         if (!multi_device(*s, p, nullptr)) {
             reserve(*s, p);

@@ -570,65 +570,84 @@ int wavefront_segments(uint32_t image_bytes, int cus) {
     return wf_in_lds(image_bytes) ? cus : cus * kGlobalBlocksPerCu;
 }
 
-hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams& wf_in, int cus, int max_bounces,
-                            hipStream_t st, hipEvent_t ev0, hipEvent_t ev1, hipEvent_t ev2, float4* fb,
-                            int* variant_out) {
+hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams* wf_in, int nwf, const WfStreams& ws, int cus,
+                            int max_bounces, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1, hipEvent_t ev2,
+                            float4* fb, int* variant_out) {
     KernelParams kp = kp_in;
     const uint32_t img = kp.scene.image_bytes;
     const bool in_lds = wf_in_lds(img);
     kp.total_lanes = (uint32_t)total_lanes_for(img, cus);
     const uint32_t nseg = (uint32_t)wavefront_segments(img, cus);
     const uint32_t per = in_lds ? 4u : 1u;                         // shade workgroups per segment
+    // Two streams (ws.st2): batches alternate between them, each stream with
+    // its own queues/counters (wf_in[1]) and stack spill area, so one batch's
+    // shade and the tail of its extend overlap the other batch's extend.
+    const bool two = nwf == 2 && ws.st2 != nullptr;
     hipError_t e = hipSuccess;
     if (ev0 && (e = hipEventRecord(ev0, st)) != hipSuccess) return e;
+    if (two) {
+        if ((e = hipEventRecord(ws.fork, st)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(ws.st2, ws.fork, 0)) != hipSuccess) return e;
+    }
+    uint32_t batch = 0;
     for (uint32_t chunk = 0; chunk < kp.nchunks;) {
-        WfParams wf = wf_in;
-        wf.nseg = nseg;
-        wf.chunk_index = chunk;
-        wf.s_begin = chunk * kp.chunk;
-        wf.nsc = (kp.spp - wf.s_begin) < kp.chunk ? (kp.spp - wf.s_begin) : kp.chunk;
         // whole-image batches may span several full chunks (fewer, longer launches)
+        const uint32_t nsc = (kp.spp - chunk * kp.chunk) < kp.chunk ? (kp.spp - chunk * kp.chunk) : kp.chunk;
         uint32_t ncb = 1;
-        if (wf.nsc == kp.chunk && (uint64_t)kp.npix_local * kp.chunk <= wf.capacity) {
+        if (nsc == kp.chunk && (uint64_t)kp.npix_local * kp.chunk <= wf_in[0].capacity) {
             const uint32_t full = (kp.spp / kp.chunk) - chunk;             // full chunks left
-            const uint32_t fit = (uint32_t)(wf.capacity / ((uint64_t)kp.npix_local * kp.chunk));
+            const uint32_t fit = (uint32_t)(wf_in[0].capacity / ((uint64_t)kp.npix_local * kp.chunk));
             ncb = fit < full ? fit : full;
         }
-        wf.ns = ncb * wf.nsc;
+        const uint32_t chunk0 = chunk;
         chunk += ncb;
-        const uint32_t nb_max = wf.capacity / wf.ns;
-        for (uint32_t v0 = 0; v0 < kp.npix_local; v0 += nb_max) {
+        const uint32_t nb_max = wf_in[0].capacity / (ncb * nsc);
+        for (uint32_t v0 = 0; v0 < kp.npix_local; v0 += nb_max, ++batch) {
+            const int h = two ? (int)(batch & 1u) : 0;
+            const hipStream_t bs = h ? ws.st2 : st;
+            KernelParams kb = kp;
+            if (h) kb.spill = kp.spill + (size_t)32 * kp.total_lanes;   // the second stream's spill area
+            WfParams wf = wf_in[h];
+            wf.nseg = nseg;
+            wf.chunk_index = chunk0;
+            wf.s_begin = chunk0 * kp.chunk;
+            wf.nsc = nsc;
+            wf.ns = ncb * nsc;
             wf.v0 = v0;
             wf.nb = (kp.npix_local - v0) < nb_max ? (kp.npix_local - v0) : nb_max;
             const uint32_t n = wf.nb * wf.ns;
             wf.group_shift = in_lds ? 6u : wf_global_group_shift();
             // whole groups per segment
             wf.seg = ((((n + (1u << wf.group_shift) - 1u) >> wf.group_shift) + nseg - 1) / nseg) << wf.group_shift;
-            e = hipMemsetAsync(wf.cnt, 0, sizeof(WfCounters) * (size_t)nseg * (size_t)(max_bounces + 1), st);
+            e = hipMemsetAsync(wf.cnt, 0, sizeof(WfCounters) * (size_t)nseg * (size_t)(max_bounces + 1), bs);
             if (e != hipSuccess) return e;
             const uint32_t gen_grid = (n + kGenBlock - 1) / kGenBlock;
             hipLaunchKernelGGL(wf_generate, dim3(gen_grid < 16u * (uint32_t)cus ? gen_grid : 16u * (uint32_t)cus),
-                               dim3(kGenBlock), 0, st, kp, wf);
+                               dim3(kGenBlock), 0, bs, kb, wf);
             if ((e = hipGetLastError()) != hipSuccess) return e;
             for (int b = 0; b < max_bounces; b++) {
                 wf.bounce = b;
                 if (in_lds)
-                    e = launch_extend<true, 4, kLdsBlock>(kp, wf, (int)nseg, lds_bytes_in_lds(img, 4) + 32, st);
+                    e = launch_extend<true, 4, kLdsBlock>(kb, wf, (int)nseg, lds_bytes_in_lds(img, 4) + 32, bs);
                 else
-                    e = launch_extend<false, 8, kGlobalBlock>(kp, wf, (int)nseg, (size_t)8 * kGlobalBlock * 16 + 32,
-                                                              st);
+                    e = launch_extend<false, 8, kGlobalBlock>(kb, wf, (int)nseg, (size_t)8 * kGlobalBlock * 16 + 32,
+                                                              bs);
                 if (e != hipSuccess) return e;
                 if (wf.sort)
-                    hipLaunchKernelGGL(wf_shade, dim3(nseg * per), dim3(kShadeBlock), 0, st, kp, wf, per);
+                    hipLaunchKernelGGL(wf_shade, dim3(nseg * per), dim3(kShadeBlock), 0, bs, kb, wf, per);
                 else if (in_lds)
-                    hipLaunchKernelGGL(wf_shade_slots<1024>, dim3(nseg), dim3(1024), 0, st, kp, wf);
+                    hipLaunchKernelGGL(wf_shade_slots<1024>, dim3(nseg), dim3(1024), 0, bs, kb, wf);
                 else
-                    hipLaunchKernelGGL(wf_shade_slots<256>, dim3(nseg), dim3(256), 0, st, kp, wf);
+                    hipLaunchKernelGGL(wf_shade_slots<256>, dim3(nseg), dim3(256), 0, bs, kb, wf);
                 if ((e = hipGetLastError()) != hipSuccess) return e;
             }
-            hipLaunchKernelGGL(wf_accumulate, dim3((wf.nb + 255u) / 256u, ncb), dim3(256), 0, st, kp, wf);
+            hipLaunchKernelGGL(wf_accumulate, dim3((wf.nb + 255u) / 256u, ncb), dim3(256), 0, bs, kb, wf);
             if ((e = hipGetLastError()) != hipSuccess) return e;
         }
+    }
+    if (two) {
+        if ((e = hipEventRecord(ws.join, ws.st2)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(st, ws.join, 0)) != hipSuccess) return e;
     }
     if (ev1 && (e = hipEventRecord(ev1, st)) != hipSuccess) return e;
     e = launch_reduce(kp, fb, st);
