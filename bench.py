@@ -377,14 +377,17 @@ def main():
                 "traffic": None, "traffic_unit": "GB of HBM read+write per path-kernel launch",
                 "source": "rocprofv3 --pmc passes of this build and workload, run by this bench"}
         if world == 1 and not args.no_pmc and args.pipeline == "wavefront":
-            # per-kernel measured HBM traffic; `achieved` = the whole pipeline's bytes / its kernels' time
+            # per-kernel measured HBM traffic; `achieved` = the whole pipeline's bytes / the frame's
+            # kernel time (HIP events of the timed renders: the streams overlap kernels, while the
+            # PMC passes serialize them, so each kernel's own ms/GBps there is its time alone)
             kh = wavefront_hbm(args)
             if kh:
                 tot_b = sum((k["hbm_read_GB"] + k["hbm_write_GB"]) for k in kh.values())
-                tot_ms = sum(k["ms"] for k in kh.values())
-                gbs = tot_b / (tot_ms * 1e-3) if tot_ms > 0 else 0.0
+                gbs = tot_b / (kern_ms * 1e-3) if kern_ms > 0 else 0.0
                 roof.update(achieved=round(gbs, 2), frac=round(gbs / HBM_PEAK_GBS, 5), traffic=round(tot_b, 3),
-                            traffic_unit="GB of HBM read+write per frame (all wavefront kernels)", kernels=kh)
+                            traffic_unit="GB of HBM read+write per frame (all wavefront kernels)", kernels=kh,
+                            kernels_note="per-kernel ms / GBps from the PMC passes, which run kernels one at a "
+                                         "time; the timed frame overlaps them on several streams")
         elif world == 1 and not args.no_pmc:
             # measured HBM bytes: FETCH_SIZE x2 (gfx950 streaming-read undercount) + WRITE_SIZE, KiB
             pmc = live_counters(args)

@@ -86,8 +86,10 @@ typedef struct {
     int32_t shard_index;
     int32_t packed;             /* 1: write owned tiles packed (tile-major) instead of row-major */
     int32_t pipeline;           /* MCPT_PIPELINE_*: megakernel (default) or wavefront; same image */
-    uint32_t wf_batch;          /* wavefront: max paths in flight per batch (160 B of device
-                                   memory each), 0 = 1<<27, 1<<28 for scenes in global memory */
+    uint32_t wf_batch;          /* wavefront: max paths per batch (160 B of device memory each,
+                                   per stream: batches rotate over 2 streams for scenes in LDS,
+                                   4 for scenes in global memory; MCPT_WF_STREAMS overrides),
+                                   0 = 1<<27 (1<<28 for a global-memory scene on one stream) */
     int32_t mode;               /* MCPT_MODE_*: path semantics (default CVMCTracer)       */
     int32_t lean;               /* 1: the megakernel counts only rays (paths, shades, spills,
                                    inner/leaf visits, leaf refs, triangle tests read 0; image and

@@ -125,8 +125,8 @@ struct mcpt_scene {
     size_t gather_bytes = 0;
     // wavefront: a second stream for every other batch, forked from and joined
     // back into the caller's stream (created on first use)
-    hipStream_t wf_stream = nullptr;
-    hipEvent_t wf_fork = nullptr, wf_join = nullptr;
+    hipStream_t wf_stream[mcpt::kMaxWfStreams] = {};   // [0] unused (the caller's)
+    hipEvent_t wf_fork = nullptr, wf_join[mcpt::kMaxWfStreams] = {};
 
     ~mcpt_scene() {
         if (!on_device) return;
@@ -138,10 +138,13 @@ struct mcpt_scene {
             if (p) (void)hipFree(p);
         for (auto& t : pending) for (auto ev : t.e) (void)hipEventDestroy(ev);
         for (auto& t : free_timing) for (auto ev : t.e) (void)hipEventDestroy(ev);
-        for (hipEvent_t ev : {done, start, wf_fork, wf_join})
+        for (hipEvent_t ev : {done, start, wf_fork})
             if (ev) (void)hipEventDestroy(ev);
+        for (int i = 0; i < mcpt::kMaxWfStreams; i++) {
+            if (wf_join[i]) (void)hipEventDestroy(wf_join[i]);
+            if (wf_stream[i]) (void)hipStreamDestroy(wf_stream[i]);
+        }
         if (stream) (void)hipStreamDestroy(stream);
-        if (wf_stream) (void)hipStreamDestroy(wf_stream);
         replicas.clear();                 // each replica frees on its own device
         if (prev >= 0) (void)hipSetDevice(prev);
     }
@@ -359,6 +362,17 @@ struct Plan {
     int32_t wf_sort;             // wavefront material sort (mcpt_render_params::wf_sort)
 };
 
+// wavefront streams: 2 for scenes in LDS, 4 for scenes in global memory (C2
+// 1024 spp, streams x batch: 2 x 2^27 11.48, 2 x 2^26 11.46, 4 x 2^27 11.52,
+// 4 x 2^26 10.93; C4 1024 spp: 1 x 2^28 6.14, 2 x 2^28 8.07, 3 x 2^27 8.17,
+// 4 x 2^27 8.28 G rays/s, means of 2-3 runs).  MCPT_WF_STREAMS=n (1..4)
+// overrides; 1 = every batch on the caller's stream.
+int wavefront_streams(const mcpt_scene& s) {
+    const char* e = std::getenv("MCPT_WF_STREAMS");
+    const int n = e ? std::atoi(e) : (s.gpu.node_boxes ? 4 : 2);
+    return n < 1 ? 1 : (n > mcpt::kMaxWfStreams ? mcpt::kMaxWfStreams : n);
+}
+
 Plan make_plan(const mcpt_scene& s, const mcpt_render_params* p) {
     if (!p) throw mcpt::Error{MCPT_E_INVALID, "params is NULL"};
     if (p->width <= 0 || p->height <= 0) throw mcpt::Error{MCPT_E_INVALID, "width/height must be positive"};
@@ -442,10 +456,12 @@ Plan make_plan(const mcpt_scene& s, const mcpt_render_params* p) {
     pl.pipeline = p->pipeline;
     pl.wf_sort = p->wf_sort ? 1 : 0;
     {
-        // default batch: big (160 B of queues per path; fewer launches, shorter
-        // relative tails).  C2 2^24 5.59, 2^25 6.43, 2^26 7.07, 2^27 7.31, 2^28 7.24;
-        // C4 (256 spp) 2^24 2.90, 2^26 3.45, 2^28 4.31 G rays/s
-        uint64_t cap = p->wf_batch ? p->wf_batch : (s.gpu.node_boxes ? (1u << 28) : (1u << 27));
+        // default batch: big (160 B of queues per path and stream; fewer launches,
+        // shorter relative tails).  One stream: C2 2^24 5.59, 2^25 6.43, 2^26 7.07,
+        // 2^27 7.31, 2^28 7.24; C4 (256 spp) 2^24 2.90, 2^26 3.45, 2^28 4.31 G
+        // rays/s.  Global-memory scenes on 4 streams: 2^27 each (see wavefront_streams)
+        const bool g1 = s.gpu.node_boxes && wavefront_streams(s) == 1;
+        uint64_t cap = p->wf_batch ? p->wf_batch : (g1 ? (1u << 28) : (1u << 27));
         cap = std::max<uint64_t>(cap, chunk);                        // at least one pixel per batch
         cap = std::min<uint64_t>(cap, std::max<uint64_t>(npix, 1) * std::max<uint64_t>(p->spp, chunk));
         cap = std::min<uint64_t>(cap, uint64_t(1) << 28);               // u32 slot arithmetic; 160 B per path
@@ -467,7 +483,7 @@ void prepare_workspace(mcpt_scene& s, mcpt::KernelParams& k, bool tail_split = f
         HIP_TRY(hipMemset(s.ws.small, 0, 256));
     }
     const size_t lanes = static_cast<size_t>(mcpt::total_lanes_for(s.gpu.image_bytes, s.cus));
-    // (the wavefront's two streams run extends concurrently: one spill area each)
+    // (the wavefront's streams run extends concurrently: one spill area each)
     ensure_buf(s.ws.spill, s.ws.spill_bytes, size_t(spill_sets) * 32 * lanes * 16);
     k.partial = static_cast<float4*>(s.ws.partial);
     k.counter = static_cast<uint32_t*>(s.ws.small);
@@ -499,12 +515,7 @@ void prepare_workspace(mcpt_scene& s, mcpt::KernelParams& k, bool tail_split = f
 
 // wavefront workspace: 2 ray queues (o, d float4), hits, 4 class lists,
 // path state and radiance, per-bounce counters -- carved from one buffer, once
-// per stream (`sets`: batches alternate between two streams, each with its own)
-int wavefront_streams() {
-    // MCPT_WF_STREAMS=1: every batch on the caller's stream (A/B and tests)
-    const char* e = std::getenv("MCPT_WF_STREAMS");
-    return e && std::atoi(e) == 1 ? 1 : 2;
-}
+// per stream (`sets`: batches rotate over the wavefront's streams, each with its own)
 
 void prepare_wavefront(mcpt_scene& s, const Plan& pl, int sets, mcpt::WfParams* out) {
     const size_t cap = pl.wf_capacity;
@@ -560,7 +571,7 @@ void render_async(mcpt_scene& s, const mcpt_render_params* p, float* d_fb, hipSt
     Plan pl = make_plan(s, p);
     pl.kp.raw_mean = raw_mean ? 1 : 0;
     // the tail split hands units out by sample, so per-unit counters need whole units
-    const int wf_sets = pl.pipeline == MCPT_PIPELINE_WAVEFRONT ? wavefront_streams() : 1;
+    const int wf_sets = pl.pipeline == MCPT_PIPELINE_WAVEFRONT ? wavefront_streams(s) : 1;
     prepare_workspace(s, pl.kp, pl.pipeline == MCPT_PIPELINE_MEGAKERNEL && !d_unit_counters, wf_sets);
     pl.kp.unit_counters = d_unit_counters;
     Timing t;
@@ -572,16 +583,23 @@ void render_async(mcpt_scene& s, const mcpt_render_params* p, float* d_fb, hipSt
     }
     if (pl.pipeline == MCPT_PIPELINE_WAVEFRONT) {
         if (d_unit_counters) throw mcpt::Error{MCPT_E_UNSUPPORTED, "unit counters need the megakernel pipeline"};
-        mcpt::WfParams wf[2];
+        mcpt::WfParams wf[mcpt::kMaxWfStreams];
         prepare_wavefront(s, pl, wf_sets, wf);
-        if (wf_sets == 2 && !s.wf_stream) {
-            HIP_TRY(hipStreamCreateWithFlags(&s.wf_stream, hipStreamNonBlocking));
-            HIP_TRY(hipEventCreateWithFlags(&s.wf_fork, hipEventDisableTiming));
-            HIP_TRY(hipEventCreateWithFlags(&s.wf_join, hipEventDisableTiming));
+        mcpt::WfStreams wst{};
+        wst.n = wf_sets;
+        wst.st[0] = st;
+        if (wf_sets > 1 && !s.wf_fork) HIP_TRY(hipEventCreateWithFlags(&s.wf_fork, hipEventDisableTiming));
+        wst.fork = s.wf_fork;
+        for (int i = 1; i < wf_sets; i++) {
+            if (!s.wf_stream[i]) {
+                HIP_TRY(hipStreamCreateWithFlags(&s.wf_stream[i], hipStreamNonBlocking));
+                HIP_TRY(hipEventCreateWithFlags(&s.wf_join[i], hipEventDisableTiming));
+            }
+            wst.st[i] = s.wf_stream[i];
+            wst.join[i] = s.wf_join[i];
         }
         const int queries = pl.kp.mode == MCPT_MODE_QUINENGINE ? 3 * pl.kp.max_depth + 1 : pl.kp.max_depth + 1;
-        const mcpt::WfStreams ws2{wf_sets == 2 ? s.wf_stream : nullptr, s.wf_fork, s.wf_join};
-        HIP_TRY(mcpt::launch_wavefront(pl.kp, wf, wf_sets, ws2, s.cus, queries, st, t.e[0], t.e[1], t.e[2],
+        HIP_TRY(mcpt::launch_wavefront(pl.kp, wf, wst, s.cus, queries, t.e[0], t.e[1], t.e[2],
                                        reinterpret_cast<float4*>(d_fb), &s.last_variant));
     } else {
         HIP_TRY(mcpt::launch_render(pl.kp, s.cus, st, t.e[0], t.e[1], t.e[2], reinterpret_cast<float4*>(d_fb),
@@ -1137,10 +1155,10 @@ int mcpt_scene_reserve(mcpt_scene* s, const mcpt_render_params* p) {
         auto reserve = [&](mcpt_scene& sc, const mcpt_render_params* q) {
             set_device(sc);
             Plan pl = make_plan(sc, q);
-            const int sets = pl.pipeline == MCPT_PIPELINE_WAVEFRONT ? wavefront_streams() : 1;
+            const int sets = pl.pipeline == MCPT_PIPELINE_WAVEFRONT ? wavefront_streams(sc) : 1;
             prepare_workspace(sc, pl.kp, pl.pipeline == MCPT_PIPELINE_MEGAKERNEL, sets);
             if (pl.pipeline == MCPT_PIPELINE_WAVEFRONT) {
-                mcpt::WfParams wf[2];
+                mcpt::WfParams wf[mcpt::kMaxWfStreams];
                 prepare_wavefront(sc, pl, sets, wf);
             }
         };

@@ -186,14 +186,16 @@ void read_lane_use_wf(unsigned long long out[6]);   // wavefront extend
 int wavefront_segments(uint32_t image_bytes, int cus);
 // wavefront pipeline: generate / extend / shade per bounce / accumulate per
 // batch, then the same reduction (events: ev0 before, ev1 after the batches)
-// second stream for every other batch (st2 null: all batches on st), with
-// the events that fork it from and join it back into st
+// wavefront streams: batch i runs on stream i mod n (st[0] = the caller's),
+// forked from and joined back into st[0] with the events of each extra stream
+constexpr int kMaxWfStreams = 4;
 struct WfStreams {
-    hipStream_t st2;
-    hipEvent_t fork, join;
+    int n;
+    hipStream_t st[kMaxWfStreams];
+    hipEvent_t fork, join[kMaxWfStreams];
 };
-hipError_t launch_wavefront(const KernelParams& kp, const WfParams* wf, int nwf, const WfStreams& ws, int cus,
-                            int max_bounces, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1, hipEvent_t ev2,
-                            float4* fb, int* variant_out);
+hipError_t launch_wavefront(const KernelParams& kp, const WfParams* wf, const WfStreams& ws, int cus,
+                            int max_bounces, hipEvent_t ev0, hipEvent_t ev1, hipEvent_t ev2, float4* fb,
+                            int* variant_out);
 
 }  // namespace mcpt

@@ -570,29 +570,31 @@ int wavefront_segments(uint32_t image_bytes, int cus) {
     return wf_in_lds(image_bytes) ? cus : cus * kGlobalBlocksPerCu;
 }
 
-hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams* wf_in, int nwf, const WfStreams& ws, int cus,
-                            int max_bounces, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1, hipEvent_t ev2,
-                            float4* fb, int* variant_out) {
+hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams* wf_in, const WfStreams& ws, int cus,
+                            int max_bounces, hipEvent_t ev0, hipEvent_t ev1, hipEvent_t ev2, float4* fb,
+                            int* variant_out) {
     KernelParams kp = kp_in;
     const uint32_t img = kp.scene.image_bytes;
     const bool in_lds = wf_in_lds(img);
     kp.total_lanes = (uint32_t)total_lanes_for(img, cus);
     const uint32_t nseg = (uint32_t)wavefront_segments(img, cus);
     const uint32_t per = in_lds ? 4u : 1u;                         // shade workgroups per segment
-    // Two streams (ws.st2): batches alternate between them, each stream with
-    // its own queues/counters (wf_in[1]) and stack spill area, so one batch's
-    // shade and the tail of its extend overlap the other batch's extend.  The
-    // shade then runs 256-thread workgroups (62 VGPRs, 4 B of LDS): one fits on
-    // a CU beside the extend's 16 waves (LDS scenes: 1024 threads, 157 KB; global
-    // scenes: 4 x 256 threads, 4 x 32 KB), so shading fills the extend's idle
-    // issue slots instead of waiting for it (C2 wavefront 10.10 -> 11.25, C4 at
-    // 1024 spp 6.14 -> 8.04 G rays/s).
-    const bool two = nwf == 2 && ws.st2 != nullptr;
+    // Several streams (ws.n > 1): batch i runs on stream i mod n, each stream
+    // with its own queues/counters (wf_in[i]) and stack spill area, so one
+    // batch's shade and the tail of its extend overlap another batch's extend.
+    // The shade then runs 256-thread workgroups (64 VGPRs, 4 B of LDS): one
+    // fits on a CU beside the extend's 16 waves (LDS scenes: 1024 threads,
+    // 157 KB; global scenes: 4 x 256 threads, 4 x 32 KB), so shading fills the
+    // extend's idle issue slots instead of waiting for it (two streams: C2
+    // wavefront 10.10 -> 11.25, C4 at 1024 spp 6.14 -> 8.04 G rays/s).
+    const int ns = ws.n < 1 ? 1 : (ws.n > kMaxWfStreams ? kMaxWfStreams : ws.n);
+    const hipStream_t st = ws.st[0];
     hipError_t e = hipSuccess;
     if (ev0 && (e = hipEventRecord(ev0, st)) != hipSuccess) return e;
-    if (two) {
+    if (ns > 1) {
         if ((e = hipEventRecord(ws.fork, st)) != hipSuccess) return e;
-        if ((e = hipStreamWaitEvent(ws.st2, ws.fork, 0)) != hipSuccess) return e;
+        for (int i = 1; i < ns; i++)
+            if ((e = hipStreamWaitEvent(ws.st[i], ws.fork, 0)) != hipSuccess) return e;
     }
     uint32_t batch = 0;
     for (uint32_t chunk = 0; chunk < kp.nchunks;) {
@@ -608,10 +610,10 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams* wf_in, in
         chunk += ncb;
         const uint32_t nb_max = wf_in[0].capacity / (ncb * nsc);
         for (uint32_t v0 = 0; v0 < kp.npix_local; v0 += nb_max, ++batch) {
-            const int h = two ? (int)(batch & 1u) : 0;
-            const hipStream_t bs = h ? ws.st2 : st;
+            const int h = (int)(batch % (uint32_t)ns);
+            const hipStream_t bs = ws.st[h];
             KernelParams kb = kp;
-            if (h) kb.spill = kp.spill + (size_t)32 * kp.total_lanes;   // the second stream's spill area
+            kb.spill = kp.spill + (size_t)h * 32 * kp.total_lanes;       // this stream's spill area
             WfParams wf = wf_in[h];
             wf.nseg = nseg;
             wf.chunk_index = chunk0;
@@ -640,7 +642,7 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams* wf_in, in
                 if (e != hipSuccess) return e;
                 if (wf.sort)
                     hipLaunchKernelGGL(wf_shade, dim3(nseg * per), dim3(kShadeBlock), 0, bs, kb, wf, per);
-                else if (in_lds && !two)   // alone on the GPU: 16 waves per segment keep HBM busy
+                else if (in_lds && ns == 1)   // alone on the GPU: 16 waves per segment keep HBM busy
                     hipLaunchKernelGGL(wf_shade_slots<1024>, dim3(nseg), dim3(1024), 0, bs, kb, wf);
                 else
                     hipLaunchKernelGGL(wf_shade_slots<256>, dim3(nseg), dim3(256), 0, bs, kb, wf);
@@ -650,9 +652,9 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams* wf_in, in
             if ((e = hipGetLastError()) != hipSuccess) return e;
         }
     }
-    if (two) {
-        if ((e = hipEventRecord(ws.join, ws.st2)) != hipSuccess) return e;
-        if ((e = hipStreamWaitEvent(st, ws.join, 0)) != hipSuccess) return e;
+    for (int i = 1; i < ns; i++) {
+        if ((e = hipEventRecord(ws.join[i], ws.st[i])) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(st, ws.join[i], 0)) != hipSuccess) return e;
     }
     if (ev1 && (e = hipEventRecord(ev1, st)) != hipSuccess) return e;
     e = launch_reduce(kp, fb, st);
