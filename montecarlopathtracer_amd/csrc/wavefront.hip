@@ -186,8 +186,11 @@ struct ClassBuf {
 };
 
 // ---- extend: closest hit of every ray of this workgroup's segment -----------
-// COUNT = false (lean renders): the traversal counters are compiled out
-template <bool IN_LDS, int S, int BLOCK, bool COUNT>
+// COUNT = false (lean renders): the traversal counters are compiled out.
+// SORT = WfParams::sort, a template argument so that the queue-order variant
+// carries no class-list buffers (8 VGPRs: the co-resident shade of the
+// multi-stream pipeline needs the extend at <= 96)
+template <bool IN_LDS, int S, int BLOCK, bool COUNT, bool SORT>
 __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const WfParams wf) {
     static_assert((BLOCK & (BLOCK - 1)) == 0, "stack slot addresses (slot_of) mask by a power-of-two block");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -306,7 +309,7 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
             // CV: scatter while depth < max_depth (CUTracer.cu:103-160); QE: while
             // bounce < 3*depth (rtx.hlsl:312), roulette is drawn in shade
             const int32_t lim = kp.mode == kModeQE ? 3 * kp.max_depth : kp.max_depth;
-            if (wf.sort && r.htri >= 0 && depth != kNoRay && (int32_t)depth < lim) {
+            if (SORT && r.htri >= 0 && depth != kNoRay && (int32_t)depth < lim) {
                 const GpuGeom& gm = geoms[__float_as_uint(tris[r.htri + 1].w)];
                 if (!is_emitter(gm)) cls = material_class(gm);
             }
@@ -318,7 +321,7 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
             }
             qb[qf(seg0 + fslot, 2, qs)] = hrec;
         }
-        if (wf.sort) {
+        if constexpr (SORT) {
 #pragma unroll
             for (uint32_t k = 0; k < 4; k++)
                 out[k].append(cls == k, fslot, lcnt + k, wf.cls_list + (size_t)k * wf.slot_stride + seg0);
@@ -333,7 +336,7 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
         WF_STAMP(tm_hand);
         if (!__ballot(mode != kDead)) break;
     }
-    if (wf.sort) {
+    if constexpr (SORT) {
 #pragma unroll
         for (uint32_t k = 0; k < 4; k++) out[k].flush(lcnt + k, wf.cls_list + (size_t)k * wf.slot_stride + seg0);
     }
@@ -537,7 +540,9 @@ __global__ void __launch_bounds__(256) wf_accumulate(const KernelParams kp, cons
 
 template <bool IN_LDS, int S, int BLOCK>
 hipError_t launch_extend(const KernelParams& kp, const WfParams& wf, int grid, size_t lds, hipStream_t st) {
-    auto kern = kp.lean ? wf_extend<IN_LDS, S, BLOCK, false> : wf_extend<IN_LDS, S, BLOCK, true>;
+    auto kern = wf.sort ? (kp.lean ? wf_extend<IN_LDS, S, BLOCK, false, true> : wf_extend<IN_LDS, S, BLOCK, true, true>)
+                        : (kp.lean ? wf_extend<IN_LDS, S, BLOCK, false, false>
+                                   : wf_extend<IN_LDS, S, BLOCK, true, false>);
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
@@ -582,11 +587,13 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams* wf_in, co
     // Several streams (ws.n > 1): batch i runs on stream i mod n, each stream
     // with its own queues/counters (wf_in[i]) and stack spill area, so one
     // batch's shade and the tail of its extend overlap another batch's extend.
-    // The shade then runs 256-thread workgroups (64 VGPRs, 4 B of LDS): one
-    // fits on a CU beside the extend's 16 waves (LDS scenes: 1024 threads,
-    // 157 KB; global scenes: 4 x 256 threads, 4 x 32 KB), so shading fills the
-    // extend's idle issue slots instead of waiting for it (two streams: C2
-    // wavefront 10.10 -> 11.25, C4 at 1024 spp 6.14 -> 8.04 G rays/s).
+    // The shade then runs in workgroups that fit on a CU beside the extend's 16
+    // waves (extend <= 88 VGPRs per lane, so 160 of the SIMD's 512 are left:
+    // two 64-VGPR shade waves; 4 B of LDS): 512 threads for LDS scenes (one
+    // 1024-thread extend workgroup with 157 KB of LDS per CU), 256 for global
+    // scenes (four 256-thread extend workgroups), so shading fills the
+    // extend's idle issue slots instead of waiting for it (C2 wavefront 10.10
+    // -> 13.20, C4 at 1024 spp 6.14 -> 8.34 G rays/s).
     const int ns = ws.n < 1 ? 1 : (ws.n > kMaxWfStreams ? kMaxWfStreams : ws.n);
     const hipStream_t st = ws.st[0];
     hipError_t e = hipSuccess;
@@ -644,6 +651,8 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams* wf_in, co
                     hipLaunchKernelGGL(wf_shade, dim3(nseg * per), dim3(kShadeBlock), 0, bs, kb, wf, per);
                 else if (in_lds && ns == 1)   // alone on the GPU: 16 waves per segment keep HBM busy
                     hipLaunchKernelGGL(wf_shade_slots<1024>, dim3(nseg), dim3(1024), 0, bs, kb, wf);
+                else if (in_lds)              // beside an extend workgroup: 8 waves (2 x 64 VGPRs per SIMD)
+                    hipLaunchKernelGGL(wf_shade_slots<512>, dim3(nseg), dim3(512), 0, bs, kb, wf);
                 else
                     hipLaunchKernelGGL(wf_shade_slots<256>, dim3(nseg), dim3(256), 0, bs, kb, wf);
                 if ((e = hipGetLastError()) != hipSuccess) return e;
