@@ -3,18 +3,22 @@
 
 One step = one full path-traced frame of the workload (every pixel, every
 sample, up to 7 scatter events + 1 terminal query per path) through the C ABI
-(mcpt_render_device), plus -- for N > 1 -- the RCCL gather of the per-rank
+(mcpt_render_device) -- by default on the wavefront pipeline, whose image is
+bit-identical to the megakernel's and which is the faster of the two on
+MI355X (N = 1 runs also time the megakernel, reported under other_pipeline)
+-- plus, for N > 1, the RCCL gather of the per-rank
 tile buffers to rank 0 and its unpermute into the image.  Pixels are sharded
 as interleaved 8x8 tiles (tile t -> rank t % N); total work is fixed, so the
 scaling is strong.  value = closest-hit queries of all ranks / max-over-ranks
 wall time (Mray/s).
 
-Roofline: `achieved` = the path kernel's MEASURED HBM bytes (rocprofv3 PMC
-passes of this build and workload, run by this bench in child processes:
-FETCH_SIZE x2 + WRITE_SIZE) / its HIP-event duration; the kernel is bound by
-VALU issue, reported under roofline.valu (issue and lane fractions from the
-same passes); SURVEY.md section 8(d)'s algorithmic bytes (LDS/L2-served) are
-reported separately under roofline.algorithmic.  Wavefront runs report each
+Roofline: `achieved` = the MEASURED HBM bytes of the frame's kernels (rocprofv3
+PMC passes of this build and workload, run by this bench in child processes:
+FETCH_SIZE x2 + WRITE_SIZE) / their HIP-event duration; the traversal (path
+kernel / wavefront extend) is bound by VALU issue and latency, reported under
+roofline.valu (issue and lane fractions from the same passes); SURVEY.md
+section 8(d)'s algorithmic bytes (LDS/L2-served) are reported separately
+under roofline.algorithmic.  Wavefront runs report each
 kernel's measured HBM traffic and rate under roofline.kernels (the queue
 streams: SURVEY 8(f)1), and every N = 1 run measures a 1 GiB device copy as
 the roofline's second denominator (roofline.peak_copy_measured).  cpu_baseline = BASELINE
@@ -132,6 +136,8 @@ def wavefront_hbm(args) -> dict:
     where this pipeline meets the HBM roofline."""
     f = pmc_pass(args, ["FETCH_SIZE"], "wf_fetch", reader=read_wf_kernels)
     w = pmc_pass(args, ["WRITE_SIZE"], "wf_write", reader=read_wf_kernels)
+    v = pmc_pass(args, ["SQ_INSTS_VALU", "SQ_THREAD_CYCLES_VALU", "SQ_ACTIVE_INST_VALU", "SQ_WAVE_CYCLES",
+                        "GRBM_GUI_ACTIVE"], "wf_valu", reader=read_wf_kernels)
     res = {}
     for cls in f:
         if cls not in w or "FETCH_SIZE" not in f[cls] or "WRITE_SIZE" not in w[cls]:
@@ -142,7 +148,27 @@ def wavefront_hbm(args) -> dict:
         res[cls] = {"hbm_read_GB": round(rd / 1e9, 3), "hbm_write_GB": round(wr / 1e9, 3), "ms": round(ns / 1e6, 3),
                     "launches": f[cls]["dispatches"],
                     "GBps": round((rd + wr) / max(ns, 1), 1), "frac": round((rd + wr) / max(ns, 1) / HBM_PEAK_GBS, 4)}
+        if cls in v:
+            res[cls]["valu_counters"] = {k: v[cls][k] for k in v[cls] if k.startswith(("SQ_", "GRBM_"))}
     return res
+
+
+def valu_block(pmc: dict, cus: int, kern_ms: float, rays: float) -> dict:
+    """The resource the traversal is bound by: VALU issue.  A wave64 VALU
+    instruction occupies its SIMD for 2 cycles (MI355X_MICROARCH.md), so
+    capacity = CUs x 4 SIMDs x cycles / 2; cycles = GRBM_GUI_ACTIVE / 8 XCDs."""
+    if not (pmc.get("SQ_INSTS_VALU") and pmc.get("GRBM_GUI_ACTIVE") and kern_ms > 0):
+        return {}
+    cycles = pmc["GRBM_GUI_ACTIVE"] / 8.0
+    issue = pmc["SQ_INSTS_VALU"] / (cus * 4 * cycles / 2.0)
+    lanes = (pmc["SQ_THREAD_CYCLES_VALU"] / (64.0 * pmc["SQ_ACTIVE_INST_VALU"])
+             if pmc.get("SQ_ACTIVE_INST_VALU") and pmc.get("SQ_THREAD_CYCLES_VALU") else None)
+    return {"issue_frac": round(issue, 4),
+            "lane_util": round(lanes, 4) if lanes is not None else None,
+            "useful_lane_frac": round(issue * lanes, 4) if lanes is not None else None,
+            "wave_instr_per_ray": round(pmc["SQ_INSTS_VALU"] / max(rays, 1), 2),
+            "clock_GHz_under_pmc": round(cycles / (kern_ms * 1e6), 3),
+            "formula": "SQ_INSTS_VALU / (CUs*4*cycles/2); lanes = SQ_THREAD_CYCLES_VALU / (64*SQ_ACTIVE_INST_VALU)"}
 
 
 def copy_bandwidth(dev, mib: int = 1024, reps: int = 10) -> dict:
@@ -256,7 +282,10 @@ def main():
     ap.add_argument("--height", type=int, default=1024)
     ap.add_argument("--spp", type=int, default=1024)
     ap.add_argument("--spp-chunk", type=int, default=32)
-    ap.add_argument("--pipeline", choices=["megakernel", "wavefront"], default="megakernel")
+    # default: the wavefront pipeline (bit-identical image; C2 13.2 vs 11.7 G rays/s on
+    # one MI355X); N = 1 runs also time the megakernel for comparison
+    ap.add_argument("--pipeline", choices=["megakernel", "wavefront"], default="wavefront")
+    ap.add_argument("--no-alt", action="store_true", help="skip the other pipeline's comparison timing (N = 1)")
     ap.add_argument("--wf-batch", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = this process's CPU share (<= 16)")
@@ -347,6 +376,26 @@ def main():
     elapsed = time.perf_counter() - t0
     st = scene.stats()   # waits for the recorded HIP events of each path-kernel launch
 
+    # the other pipeline on the same frame, for comparison (N = 1; same image, bit for bit)
+    alt = None
+    if world == 1 and not args.no_alt:
+        other = "megakernel" if args.pipeline == "wavefront" else "wavefront"
+        pa = dataclasses.replace(p, pipeline=other)
+        for _ in range(max(args.warmup, 1)):
+            scene.render_device(pa, fb.data_ptr(), stream.cuda_stream)
+        torch.cuda.synchronize(dev)
+        scene.stats()
+        ta = time.perf_counter()
+        for _ in range(args.steps):
+            scene.render_device(pa, fb.data_ptr(), stream.cuda_stream)
+        torch.cuda.synchronize(dev)
+        ta = time.perf_counter() - ta
+        sa = scene.stats()
+        alt = {"pipeline": other, "value": round(sa["rays"] / ta / 1e6, 3), "unit": "Mray/s",
+               "ms_per_step": round(ta / args.steps * 1e3, 3),
+               "kernel_ms_avg": round(sa["kernel_ms"] / max(sa["renders"], 1), 3),
+               "rays_equal": sa["rays"] == st["rays"]}
+
     # per-render node/leaf/triangle counts: the counting render's (identical for a lean one)
     renders = max(st["renders"], 1)
     for k in ("paths", "inner_visits", "leaf_visits", "leaf_refs", "tri_tests", "shades", "stack_spills"):
@@ -388,6 +437,14 @@ def main():
                             traffic_unit="GB of HBM read+write per frame (all wavefront kernels)", kernels=kh,
                             kernels_note="per-kernel ms / GBps from the PMC passes, which run kernels one at a "
                                          "time; the timed frame overlaps them on several streams")
+                ext = kh.get("extend", {})
+                vb = valu_block(ext.pop("valu_counters", {}), torch.cuda.get_device_properties(dev).multi_processor_count,
+                                ext.get("ms", 0.0), per_launch["rays"])
+                for k in kh.values():
+                    k.pop("valu_counters", None)
+                if vb:
+                    vb["kernel"] = "wf_extend (the traversal: the dominant kernel), run alone"
+                    roof["valu"] = vb
         elif world == 1 and not args.no_pmc:
             # measured HBM bytes: FETCH_SIZE x2 (gfx950 streaming-read undercount) + WRITE_SIZE, KiB
             pmc = live_counters(args)
@@ -397,22 +454,10 @@ def main():
                 roof.update(achieved=round(gbs, 2), frac=round(gbs / HBM_PEAK_GBS, 5), traffic=round(hbm / 1e9, 3),
                             hbm_read_GB=round(2.0 * pmc["FETCH_SIZE"] * 1024 / 1e9, 3),
                             hbm_write_GB=round(pmc["WRITE_SIZE"] * 1024 / 1e9, 3))
-            if pmc.get("SQ_INSTS_VALU") and pmc.get("GRBM_GUI_ACTIVE"):
-                # the resource the kernel is bound by: VALU issue.  A wave64 VALU
-                # instruction occupies its SIMD for 2 cycles (MI355X_MICROARCH.md), so
-                # capacity = CUs x 4 SIMDs x cycles / 2; cycles = GRBM_GUI_ACTIVE / 8 XCDs
-                cus = torch.cuda.get_device_properties(dev).multi_processor_count
-                cycles = pmc["GRBM_GUI_ACTIVE"] / 8.0
-                issue = pmc["SQ_INSTS_VALU"] / (cus * 4 * cycles / 2.0)
-                lanes = (pmc["SQ_THREAD_CYCLES_VALU"] / (64.0 * pmc["SQ_ACTIVE_INST_VALU"])
-                         if pmc.get("SQ_ACTIVE_INST_VALU") else None)
-                roof["valu"] = {"issue_frac": round(issue, 4),
-                                "lane_util": round(lanes, 4) if lanes is not None else None,
-                                "useful_lane_frac": round(issue * lanes, 4) if lanes is not None else None,
-                                "wave_instr_per_ray": round(pmc["SQ_INSTS_VALU"] / max(per_launch["rays"], 1), 2),
-                                "clock_GHz_under_pmc": round(cycles / (kern_ms * 1e6), 3),
-                                "formula": "SQ_INSTS_VALU / (CUs*4*cycles/2); lanes = SQ_THREAD_CYCLES_VALU / "
-                                           "(64*SQ_ACTIVE_INST_VALU)"}
+            vb = valu_block(pmc, torch.cuda.get_device_properties(dev).multi_processor_count, kern_ms,
+                            per_launch["rays"])
+            if vb:
+                roof["valu"] = vb
         if world == 1:
             cb = copy_bandwidth(dev)
             if roof["achieved"] is not None and cb["GBps"] > 0:
@@ -456,6 +501,7 @@ def main():
             "gpu_ms_per_step_event": round(ev0.elapsed_time(ev1) / args.steps, 3),
             "roofline": roof,
             "cpu_baseline": None,
+            "other_pipeline": alt,
         }
         if world == 1 and not args.no_cpu_baseline:
             # the GPU's own C1 frame, for the ray-count check of the CPU run

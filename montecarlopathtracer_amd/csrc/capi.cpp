@@ -460,10 +460,16 @@ Plan make_plan(const mcpt_scene& s, const mcpt_render_params* p) {
         // shorter relative tails).  One stream: C2 2^24 5.59, 2^25 6.43, 2^26 7.07,
         // 2^27 7.31, 2^28 7.24; C4 (256 spp) 2^24 2.90, 2^26 3.45, 2^28 4.31 G
         // rays/s.  Global-memory scenes on 4 streams: 2^27 each (see wavefront_streams)
-        const bool g1 = s.gpu.node_boxes && wavefront_streams(s) == 1;
+        const int nstr = wavefront_streams(s);
+        const bool g1 = s.gpu.node_boxes && nstr == 1;
         uint64_t cap = p->wf_batch ? p->wf_batch : (g1 ? (1u << 28) : (1u << 27));
+        const uint64_t work = std::max<uint64_t>(npix, 1) * std::max<uint64_t>(p->spp, chunk);
+        // a default batch gives every stream a batch of its own (one rank's C2
+        // share at 8 GPUs, 2^27 paths: one 2^27 batch 9.26, two 2^26 12.61, four
+        // 2^25 12.13 G rays/s; the megakernel 11.22)
+        if (!p->wf_batch && nstr > 1) cap = std::min<uint64_t>(cap, (work + nstr - 1) / nstr);
         cap = std::max<uint64_t>(cap, chunk);                        // at least one pixel per batch
-        cap = std::min<uint64_t>(cap, std::max<uint64_t>(npix, 1) * std::max<uint64_t>(p->spp, chunk));
+        cap = std::min<uint64_t>(cap, work);
         cap = std::min<uint64_t>(cap, uint64_t(1) << 28);               // u32 slot arithmetic; 160 B per path
         pl.wf_capacity = static_cast<uint32_t>(cap);
     }

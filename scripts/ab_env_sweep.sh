@@ -4,7 +4,7 @@
 set -e
 for round in 1 2; do
 for v in $VALS; do
-  env $VAR=$v timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-pmc $ARGS > gpurun_out/abe.log 2>gpurun_out/abe.err
+  env $VAR=$v timeout -k 10 300 python bench.py --pipeline megakernel --steps 2 --warmup 1 --no-cpu-baseline --no-pmc --no-alt $ARGS > gpurun_out/abe.log 2>gpurun_out/abe.err
   echo "round $round $VAR=$v: $(grep -o '"value": [0-9.]*' gpurun_out/abe.log)"
 done
 done

@@ -6,7 +6,7 @@ for lib in $LIBS; do
 done
 for round in 1 2; do
 for lib in $LIBS; do
-  MCPT_LIB_PATH=$PWD/montecarlopathtracer_amd/lib/$lib timeout -k 10 200 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-pmc > gpurun_out/ab_$lib.log 2>&1
+  MCPT_LIB_PATH=$PWD/montecarlopathtracer_amd/lib/$lib timeout -k 10 200 python bench.py --pipeline megakernel --no-alt --steps 2 --warmup 1 --no-cpu-baseline --no-pmc > gpurun_out/ab_$lib.log 2>&1
   echo "round $round $lib: $(grep -o '"value": [0-9.]*' gpurun_out/ab_$lib.log | head -1) $(grep -o '"stack_spills_per_ray": [0-9.]*' gpurun_out/ab_$lib.log)"
 done
 done

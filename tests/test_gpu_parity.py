@@ -128,16 +128,20 @@ def test_pw_tracer_adapter_matches_abi(mcpt, tmp_path):
     assert np.array_equal(got, host)
 
 
+@pytest.mark.parametrize("streams", ["1", "2", "3", "4"])
 @pytest.mark.parametrize("batch", [1000, 4096, 20000, 0, 1 << 22])
-def test_wavefront_batches_equal_megakernel(mcpt, batch):
+def test_wavefront_batches_equal_megakernel(mcpt, monkeypatch, batch, streams):
     """Any batch split of the wavefront (partial batches, batches spanning
-    several chunks, ragged last chunk, shards) renders the megakernel's image
-    and counts bit for bit."""
+    several chunks, ragged last chunk, shards, packed shard output) on any
+    number of streams renders the megakernel's image and counts bit for bit."""
+    monkeypatch.setenv("MCPT_WF_STREAMS", streams)
     path = mcpt.scene_path("scene01")
     scene = mcpt.Scene(mcpt.ObjModel(path))
     for kw in ({"width": 61, "height": 45, "spp": 7, "spp_chunk": 3},
                {"width": 40, "height": 24, "spp": 12, "spp_chunk": 2},
-               {"width": 64, "height": 64, "spp": 5, "spp_chunk": 5, "shard_count": 3, "shard_index": 1}):
+               {"width": 64, "height": 64, "spp": 5, "spp_chunk": 5, "shard_count": 3, "shard_index": 1},
+               {"width": 72, "height": 40, "spp": 9, "spp_chunk": 2, "shard_count": 4, "shard_index": 3,
+                "packed": True, "tile": 8}):
         mk, smk = scene.render(mcpt.RenderParams(**kw))
         wf, swf = scene.render(mcpt.RenderParams(pipeline="wavefront", wf_batch=batch, **kw))
         assert np.array_equal(mk, wf)
