@@ -466,10 +466,16 @@ def main():
             for k in roof.get("kernels", {}).values():
                 k["frac_of_copy"] = round(k["GBps"] / cb["GBps"], 4) if cb["GBps"] > 0 else None
         in_lds = st["variant"] in (1, 2, 4)   # kernel variants that hold the scene image in LDS
-        roof["binding_resource"] = (("VALU issue and lane divergence (the scene image is LDS-resident; HBM "
-                                     "carries only seeds, spills and the framebuffer)") if in_lds else
-                                    ("memory latency of the node / triangle reads (scene image in global memory, "
-                                     "served by L1/L2/MALL; profiles/r02/c4_mem)"))
+        if not in_lds:
+            roof["binding_resource"] = ("memory latency of the node / triangle reads (scene image in global memory, "
+                                        "served by L1/L2/MALL; profiles/r02/c4_mem)")
+        elif args.pipeline == "wavefront":
+            roof["binding_resource"] = ("extend (the traversal): VALU issue and lane divergence, scene image in LDS; "
+                                        "HBM carries the SoA queue streams, which generate / shade / accumulate "
+                                        "move at 60-100% of the measured copy rate beside the extend")
+        else:
+            roof["binding_resource"] = ("VALU issue and lane divergence (the scene image is LDS-resident; HBM "
+                                        "carries only stack spills and the framebuffer partials)")
         roof["algorithmic"] = {"GBps": round(algo_gbs, 1), "bytes_per_ray": round(ab["survey"] / max(per_launch["rays"], 1), 1),
                                "bytes_per_launch": int(ab["survey"]),
                                "model": "SURVEY 8(d): 32*nodes+4*leafrefs+48*tris+96*shades+16*px",

@@ -83,6 +83,31 @@ __device__ __forceinline__ size_t qf(uint32_t slot, uint32_t k, uint32_t stride)
 }
 __device__ __forceinline__ V3 xyz(float4 v) { return v3(v.x, v.y, v.z); }
 
+// Queue streams are touched once per bounce: MCPT_WF_NT marks the streaming
+// reads (bit 0) and writes (bit 1) of generate, shade and extend's ray reads
+// non-temporal so that they do not push extend's partially written hit lines
+// out of the L2.
+#ifndef MCPT_WF_NT
+#define MCPT_WF_NT 0
+#endif
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ldq(const float4* p) {
+#if MCPT_WF_NT & 1
+    const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+#else
+    return *p;
+#endif
+}
+__device__ __forceinline__ void stq(float4* p, float4 v) {
+#if MCPT_WF_NT & 2
+    const f32x4 x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<f32x4*>(p));
+#else
+    *p = v;
+#endif
+}
+
 // Group k of block b (b-th run of nseg consecutive groups) -> its segment:
 // every block deals one group to each segment, rotated by a hash of b.  With
 // a plain k -> k (an image of 2^14 8x8 tiles, 256 segments) each segment got
@@ -131,13 +156,13 @@ __global__ void __launch_bounds__(kGenBlock) wf_generate(const KernelParams kp, 
                 primary_ray_qe(kp, pix, px, py, wf.s_begin + s_local, sd, o, d);
             else
                 primary_ray(kp, pix, px, py, wf.s_begin + s_local, sd, d);
-            wf.q[0][qf(slot, 3, wf.slot_stride)] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(sd));
+            stq(&wf.q[0][qf(slot, 3, wf.slot_stride)], make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(sd)));
             c.paths++;
             c.rays++;
             depth = 0;
         }
-        wf.q[0][qf(slot, 0, wf.slot_stride)] = pack(o, pid);
-        wf.q[0][qf(slot, 1, wf.slot_stride)] = pack(d, depth);
+        stq(&wf.q[0][qf(slot, 0, wf.slot_stride)], pack(o, pid));
+        stq(&wf.q[0][qf(slot, 1, wf.slot_stride)], pack(d, depth));
     }
     flush_counters(c, kp.stats);
 }
@@ -268,8 +293,8 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
 #else
 #define WF_STAMP(acc) do {} while (0)
 #endif
-    if (slot < count) start(qb[qf(seg0 + slot, 0, qs)], qb[qf(seg0 + slot, 1, qs)]);
-    if (nslot < count) { no4 = qb[qf(seg0 + nslot, 0, qs)]; nd4 = qb[qf(seg0 + nslot, 1, qs)]; }
+    if (slot < count) start(ldq(&qb[qf(seg0 + slot, 0, qs)]), ldq(&qb[qf(seg0 + slot, 1, qs)]));
+    if (nslot < count) { no4 = ldq(&qb[qf(seg0 + nslot, 0, qs)]); nd4 = ldq(&qb[qf(seg0 + nslot, 1, qs)]); }
     WF_STAMP(tm_setup);
     for (;;) {
         // ---- traversal burst until enough lanes are done ---------------------
@@ -331,7 +356,7 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
         const uint32_t ns = cur_chunk.take(want, lcnt + 4);
         if (want) {
             nslot = ns;
-            if (nslot < count) { no4 = qb[qf(seg0 + nslot, 0, qs)]; nd4 = qb[qf(seg0 + nslot, 1, qs)]; }
+            if (nslot < count) { no4 = ldq(&qb[qf(seg0 + nslot, 0, qs)]); nd4 = ldq(&qb[qf(seg0 + nslot, 1, qs)]); }
         }
         WF_STAMP(tm_hand);
         if (!__ballot(mode != kDead)) break;
@@ -470,7 +495,8 @@ __global__ void __launch_bounds__(BLOCK) wf_shade_slots(const KernelParams kp, c
         V3 o = v3(0, 0, 0), d = v3(0, 0, 0), color = v3(0, 0, 0);
         if (i < total) {
             const size_t js = seg0 + i;
-            const float4 o4 = qb[qf(js, 0, qs)], d4 = qb[qf(js, 1, qs)], h = qb[qf(js, 2, qs)], ps = qb[qf(js, 3, qs)];
+            const float4 o4 = ldq(&qb[qf(js, 0, qs)]), d4 = ldq(&qb[qf(js, 1, qs)]), h = ldq(&qb[qf(js, 2, qs)]),
+                         ps = ldq(&qb[qf(js, 3, qs)]);
             pid = __float_as_uint(o4.w);
             depth = __float_as_uint(d4.w);
             const int32_t htri = __float_as_int(h.w);
@@ -504,7 +530,7 @@ __global__ void __launch_bounds__(BLOCK) wf_shade_slots(const KernelParams kp, c
                     c.rays++;
                 }
             }
-            if (term) wf.radiance[pid] = make_float4(L.x, L.y, L.z, 0.0f);   // (kNoRay slots: 0)
+            if (term) stq(&wf.radiance[pid], make_float4(L.x, L.y, L.z, 0.0f));   // (kNoRay slots: 0)
         }
         // next ray: the wave's continuing lanes take consecutive slots of queue b+1
         const uint64_t m = __ballot(cont);
@@ -515,9 +541,9 @@ __global__ void __launch_bounds__(BLOCK) wf_shade_slots(const KernelParams kp, c
             b0 = __shfl(b0, leader);
             if (cont) {
                 const size_t ji = seg0 + b0 + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-                qb2[qf(ji, 0, qs)] = pack(o, pid);
-                qb2[qf(ji, 1, qs)] = pack(d, depth + 1u);
-                qb2[qf(ji, 3, qs)] = pack(color, sd);
+                stq(&qb2[qf(ji, 0, qs)], pack(o, pid));
+                stq(&qb2[qf(ji, 1, qs)], pack(d, depth + 1u));
+                stq(&qb2[qf(ji, 3, qs)], pack(color, sd));
             }
         }
     }
