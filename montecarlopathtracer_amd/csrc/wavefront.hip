@@ -5,7 +5,10 @@
 // queues in HBM so that every kernel does one kind of work:
 //   generate    one primary ray per (pixel, sample) of the batch into ray
 //               queue 0, path groups (an 8x8 tile; 256 tiles for scenes in
-//               global memory) dealt to the segments round-robin
+//               global memory) dealt to the segments round-robin; in CV mode
+//               with queue-order shading only the direction stream is
+//               written (MCPT_WF_IMPLICIT0: the origin is the eye, and bounce
+//               0's shade recomputes the path state from the slot)
 //   extend b    closest hit of every ray in queue b: one persistent workgroup
 //               per queue segment, scene image in LDS (or global); waves
 //               reserve slots 64 at a time from an LDS counter, each lane
@@ -85,10 +88,11 @@ __device__ __forceinline__ V3 xyz(float4 v) { return v3(v.x, v.y, v.z); }
 
 // Queue streams are touched once per bounce: MCPT_WF_NT marks the streaming
 // reads (bit 0) and writes (bit 1) of generate, shade and extend's ray reads
-// non-temporal so that they do not push extend's partially written hit lines
-// out of the L2.
+// (bit 2: also extend's hit writes) non-temporal, so that they do not push
+// extend's partially written hit lines out of the L2.  Default 3 (C2
+// wavefront +3.5%, C4 +2%; with bit 2 as well: C2 +2%, C4 +2.8%).
 #ifndef MCPT_WF_NT
-#define MCPT_WF_NT 0
+#define MCPT_WF_NT 3
 #endif
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ float4 ldq(const float4* p) {
@@ -98,6 +102,10 @@ __device__ __forceinline__ float4 ldq(const float4* p) {
 #else
     return *p;
 #endif
+}
+__device__ __forceinline__ void stq_nt(float4* p, float4 v) {
+    const f32x4 x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<f32x4*>(p));
 }
 __device__ __forceinline__ void stq(float4* p, float4 v) {
 #if MCPT_WF_NT & 2
@@ -117,6 +125,27 @@ __device__ __forceinline__ uint32_t seg_of(uint32_t k, uint32_t b, uint32_t nseg
     const uint32_t rot = (uint32_t)(((uint64_t)(b * 2654435761u) * nseg) >> 32);
     const uint32_t g = k + rot;
     return g >= nseg ? g - nseg : g;
+}
+
+// Inverse of generate's dealing: path id of local slot j of segment g's queue 0.
+__device__ __forceinline__ uint32_t slot_pid(const WfParams& wf, uint32_t g, uint32_t j) {
+    const uint32_t gs = wf.group_shift, blk = j >> gs;
+    const uint32_t rot = seg_of(0, blk, wf.nseg);
+    const uint32_t k = g >= rot ? g - rot : g + wf.nseg - rot;
+    return ((blk * wf.nseg + k) << gs) | (j & ((1u << gs) - 1u));
+}
+
+// MCPT_WF_IMPLICIT0 = 1: bounce 0's shade (queue order, CV mode) recomputes a
+// primary ray's origin, direction and RNG state from its slot instead of
+// reading them, and generate skips the {throughput, rng} stream (64 B of
+// queue traffic less per path); 2 (default): also the {o, pid} stream
+// (extend's bounce-0 origins are the eye; 32 B more).  With MCPT_WF_NT = 3:
+// level 1 C2 wavefront +0.3%, level 2 +0.9% (C4 +1.4%).
+#ifndef MCPT_WF_IMPLICIT0
+#define MCPT_WF_IMPLICIT0 2
+#endif
+__device__ __forceinline__ bool implicit0(const KernelParams& kp, const WfParams& wf) {
+    return MCPT_WF_IMPLICIT0 && !wf.sort && kp.mode != kModeQE;
 }
 
 // ---- generate: primary rays of the batch (CUTracer.cu:186-211) -------------
@@ -156,12 +185,13 @@ __global__ void __launch_bounds__(kGenBlock) wf_generate(const KernelParams kp, 
                 primary_ray_qe(kp, pix, px, py, wf.s_begin + s_local, sd, o, d);
             else
                 primary_ray(kp, pix, px, py, wf.s_begin + s_local, sd, d);
-            stq(&wf.q[0][qf(slot, 3, wf.slot_stride)], make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(sd)));
+            if (!implicit0(kp, wf))
+                stq(&wf.q[0][qf(slot, 3, wf.slot_stride)], make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(sd)));
             c.paths++;
             c.rays++;
             depth = 0;
         }
-        stq(&wf.q[0][qf(slot, 0, wf.slot_stride)], pack(o, pid));
+        if (!(MCPT_WF_IMPLICIT0 >= 2 && implicit0(kp, wf))) stq(&wf.q[0][qf(slot, 0, wf.slot_stride)], pack(o, pid));
         stq(&wf.q[0][qf(slot, 1, wf.slot_stride)], pack(d, depth));
     }
     flush_counters(c, kp.stats);
@@ -293,8 +323,12 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
 #else
 #define WF_STAMP(acc) do {} while (0)
 #endif
-    if (slot < count) start(ldq(&qb[qf(seg0 + slot, 0, qs)]), ldq(&qb[qf(seg0 + slot, 1, qs)]));
-    if (nslot < count) { no4 = ldq(&qb[qf(seg0 + nslot, 0, qs)]); nd4 = ldq(&qb[qf(seg0 + nslot, 1, qs)]); }
+    // MCPT_WF_IMPLICIT0 >= 2: bounce 0's origins are the eye (CV mode), not read
+    const bool eye0 = MCPT_WF_IMPLICIT0 >= 2 && wf.bounce == 0 && implicit0(kp, wf);
+    const float4 eye4 = make_float4(kp.eye[0], kp.eye[1], kp.eye[2], 0.0f);
+    auto ld_o = [&](uint32_t sl) { return eye0 ? eye4 : ldq(&qb[qf(seg0 + sl, 0, qs)]); };
+    if (slot < count) start(ld_o(slot), ldq(&qb[qf(seg0 + slot, 1, qs)]));
+    if (nslot < count) { no4 = ld_o(nslot); nd4 = ldq(&qb[qf(seg0 + nslot, 1, qs)]); }
     WF_STAMP(tm_setup);
     for (;;) {
         // ---- traversal burst until enough lanes are done ---------------------
@@ -344,7 +378,11 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
             } else {
                 mode = kDead;
             }
+#if MCPT_WF_NT & 4
+            stq_nt(&qb[qf(seg0 + fslot, 2, qs)], hrec);
+#else
             qb[qf(seg0 + fslot, 2, qs)] = hrec;
+#endif
         }
         if constexpr (SORT) {
 #pragma unroll
@@ -356,7 +394,7 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
         const uint32_t ns = cur_chunk.take(want, lcnt + 4);
         if (want) {
             nslot = ns;
-            if (nslot < count) { no4 = ldq(&qb[qf(seg0 + nslot, 0, qs)]); nd4 = ldq(&qb[qf(seg0 + nslot, 1, qs)]); }
+            if (nslot < count) { no4 = ld_o(nslot); nd4 = ldq(&qb[qf(seg0 + nslot, 1, qs)]); }
         }
         WF_STAMP(tm_hand);
         if (!__ballot(mode != kDead)) break;
@@ -486,6 +524,7 @@ __global__ void __launch_bounds__(BLOCK) wf_shade_slots(const KernelParams kp, c
     float4* qb2 = wf.q[(wf.bounce + 1) & 1];
     const uint32_t qs = wf.slot_stride;
     const bool qe = kp.mode == kModeQE;
+    const bool imp = wf.bounce == 0 && implicit0(kp, wf);
     const int lane = (int)(threadIdx.x & 63u);
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0};
     for (uint32_t base = 0; base < total; base += BLOCK) {      // block-uniform trip count
@@ -495,11 +534,32 @@ __global__ void __launch_bounds__(BLOCK) wf_shade_slots(const KernelParams kp, c
         V3 o = v3(0, 0, 0), d = v3(0, 0, 0), color = v3(0, 0, 0);
         if (i < total) {
             const size_t js = seg0 + i;
-            const float4 o4 = ldq(&qb[qf(js, 0, qs)]), d4 = ldq(&qb[qf(js, 1, qs)]), h = ldq(&qb[qf(js, 2, qs)]),
-                         ps = ldq(&qb[qf(js, 3, qs)]);
+            const float4 h = ldq(&qb[qf(js, 2, qs)]);
+            const int32_t htri = __float_as_int(h.w);
+            float4 o4, d4, ps;
+            if (imp) {   // generate's primary ray, recomputed (a miss or an empty slot needs only pid)
+                pid = slot_pid(wf, g, i);
+                o4 = make_float4(kp.eye[0], kp.eye[1], kp.eye[2], __uint_as_float(pid));
+                d4 = make_float4(0, 0, 0, 0);
+                ps = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
+                if (htri >= 0) {
+                    const uint32_t s_local = pid / wf.nb;
+                    int px, py;
+                    (void)unit_pixel(kp, wf.v0 + (pid - s_local * wf.nb), px, py);
+                    uint32_t sd0;
+                    V3 d0;
+                    primary_ray(kp, (uint32_t)py * (uint32_t)kp.width + (uint32_t)px, px, py, wf.s_begin + s_local,
+                                sd0, d0);
+                    d4 = pack(d0, 0u);
+                    ps.w = __uint_as_float(sd0);
+                }
+            } else {
+                o4 = ldq(&qb[qf(js, 0, qs)]);
+                d4 = ldq(&qb[qf(js, 1, qs)]);
+                ps = ldq(&qb[qf(js, 3, qs)]);
+            }
             pid = __float_as_uint(o4.w);
             depth = __float_as_uint(d4.w);
-            const int32_t htri = __float_as_int(h.w);
             color = xyz(ps);
             sd = __float_as_uint(ps.w);
             // CV: miss -> 0; emitter -> color*Ka*ILLUM (:111-113); terminal query
