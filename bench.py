@@ -472,7 +472,7 @@ def main():
         elif args.pipeline == "wavefront":
             roof["binding_resource"] = ("extend (the traversal): VALU issue and lane divergence, scene image in LDS; "
                                         "HBM carries the SoA queue streams, which generate / shade / accumulate "
-                                        "move at 60-100% of the measured copy rate beside the extend")
+                                        "move at 55-100% of the measured copy rate beside the extend")
         else:
             roof["binding_resource"] = ("VALU issue and lane divergence (the scene image is LDS-resident; HBM "
                                         "carries only stack spills and the framebuffer partials)")
