@@ -459,10 +459,12 @@ Plan make_plan(const mcpt_scene& s, const mcpt_render_params* p) {
         // default batch: big (160 B of queues per path and stream; fewer launches,
         // shorter relative tails).  One stream: C2 2^24 5.59, 2^25 6.43, 2^26 7.07,
         // 2^27 7.31, 2^28 7.24; C4 (256 spp) 2^24 2.90, 2^26 3.45, 2^28 4.31 G
-        // rays/s.  Global-memory scenes on 4 streams: 2^27 each (see wavefront_streams)
+        // rays/s.  Global-memory scenes on 4 streams: 2^27 each (see wavefront_streams);
+        // LDS scenes on 2 streams: 2^28 each (C2 2 x 2^27 12.90, 2 x 2^28 13.03,
+        // 3 x 2^27 13.06, 4 x 2^27 12.55 G rays/s, two rounds each; 86 GB of queues)
         const int nstr = wavefront_streams(s);
-        const bool g1 = s.gpu.node_boxes && nstr == 1;
-        uint64_t cap = p->wf_batch ? p->wf_batch : (g1 ? (1u << 28) : (1u << 27));
+        const bool big = !s.gpu.node_boxes || nstr == 1;
+        uint64_t cap = p->wf_batch ? p->wf_batch : (big ? (1u << 28) : (1u << 27));
         const uint64_t work = std::max<uint64_t>(npix, 1) * std::max<uint64_t>(p->spp, chunk);
         // a default batch gives every stream a batch of its own (one rank's C2
         // share at 8 GPUs, 2^27 paths: one 2^27 batch 9.26, two 2^26 12.61, four
