@@ -163,18 +163,23 @@ __device__ __forceinline__ bool tri_prefilter(const RayState& r, const float4 A0
     const bool mags_ok = !(xb + xg > adet) & !(xt > r.best * adet);
     return signs_ok & mags_ok;
 }
-// the exact tail (IEEE quotients, CUTracer.cu:84-92) of a triangle whose prefilter passed
-__device__ __forceinline__ void tri_accept(RayState& r, const TriDets& q, uint32_t prio, uint32_t k) {
+// the IEEE quotients of the Cramer test (CUTracer.cu:84-92)
+__device__ __forceinline__ void tri_quotients(const TriDets& q, float& beta, float& gamma, float& t) {
 #if MCPT_SHARED_DIV
     const double rA = recip_shared(q.detA);
-    const float beta = div_shared(q.qb, rA);
-    const float gamma = div_shared(q.qg, rA);
-    const float t = div_shared(q.qt, rA);
+    beta = div_shared(q.qb, rA);
+    gamma = div_shared(q.qg, rA);
+    t = div_shared(q.qt, rA);
 #else
-    const float beta = q.qb / q.detA;
-    const float gamma = q.qg / q.detA;
-    const float t = q.qt / q.detA;
+    beta = q.qb / q.detA;
+    gamma = q.qg / q.detA;
+    t = q.qt / q.detA;
 #endif
+}
+// the exact tail of a triangle whose prefilter passed
+__device__ __forceinline__ void tri_accept(RayState& r, const TriDets& q, uint32_t prio, uint32_t k) {
+    float beta, gamma, t;
+    tri_quotients(q, beta, gamma, t);
     if (beta + gamma < 1.0f && beta > 0.0f && gamma > 0.0f && t > 0.0f &&
         (t < r.best || (t == r.best && prio < r.bprio))) {
         r.best = t;
@@ -183,6 +188,19 @@ __device__ __forceinline__ void tri_accept(RayState& r, const TriDets& q, uint32
         r.hbeta = beta;
         r.hgamma = gamma;
     }
+}
+// (t, beta, gamma) of ray (o, d) against the triangle record A0..A2: the same
+// operations as the traversal's accepted hit, so a hit recomputed from the
+// triangle id is bit-identical to the one the traversal found
+__device__ __forceinline__ void tri_hit_params(V3 o, V3 d, const float4 A0, const float4 A1, const float4 A2,
+                                               float& t, float& beta, float& gamma) {
+    RayState r;
+    r.o = o;
+    r.d = d;
+    r.best = 0.0f;
+    TriDets q;
+    (void)tri_prefilter(r, A0, A1, A2, q);
+    tri_quotients(q, beta, gamma, t);
 }
 __device__ __forceinline__ void test_tri_v(RayState& r, const float4 A0, const float4 A1, const float4 A2, uint32_t k) {
     TriDets q;
