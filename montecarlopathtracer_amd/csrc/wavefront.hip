@@ -152,13 +152,6 @@ __device__ __forceinline__ uint32_t slot_pid(const WfParams& wf, uint32_t g, uin
 __device__ __forceinline__ bool implicit0(const KernelParams& kp, const WfParams& wf) {
     return MCPT_WF_IMPLICIT0 && !wf.sort && kp.mode != kModeQE;
 }
-// MCPT_WF_HIT_ID = 1 (queue order): extend writes only the hit triangle's id
-// (4 B, the first quarter of the hit stream as u32) and shade recomputes t,
-// beta, gamma of a scattering ray from it (tri_hit_params: bit-identical)
-#ifndef MCPT_WF_HIT_ID
-#define MCPT_WF_HIT_ID 0
-#endif
-static_assert(MCPT_WF_SOA || !MCPT_WF_HIT_ID, "hit ids use the SoA hit stream");
 
 // ---- generate: primary rays of the batch (CUTracer.cu:186-211) -------------
 // Paths go to segments in groups of 2^group_shift (64 = one 8x8 tile of one
@@ -390,9 +383,7 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
             } else {
                 mode = kDead;
             }
-            if constexpr (MCPT_WF_HIT_ID && !SORT)
-                reinterpret_cast<int32_t*>(qb + qf(0, 2, qs))[seg0 + fslot] = r.htri;
-            else if constexpr ((MCPT_WF_NT & 4) != 0 || (!IN_LDS && MCPT_WF_NT_HIT_GLOBAL))
+            if constexpr ((MCPT_WF_NT & 4) != 0 || (!IN_LDS && MCPT_WF_NT_HIT_GLOBAL))
                 stq_nt(&qb[qf(seg0 + fslot, 2, qs)], hrec);
             else
                 qb[qf(seg0 + fslot, 2, qs)] = hrec;
@@ -547,13 +538,8 @@ __global__ void __launch_bounds__(BLOCK) wf_shade_slots(const KernelParams kp, c
         V3 o = v3(0, 0, 0), d = v3(0, 0, 0), color = v3(0, 0, 0);
         if (i < total) {
             const size_t js = seg0 + i;
-#if MCPT_WF_HIT_ID
-            const int32_t htri = reinterpret_cast<const int32_t*>(qb + qf(0, 2, qs))[js];
-            float4 h = make_float4(0, 0, 0, 0);
-#else
             const float4 h = ldq(&qb[qf(js, 2, qs)]);
             const int32_t htri = __float_as_int(h.w);
-#endif
             float4 o4, d4, ps;
             if (imp) {   // generate's primary ray, recomputed (a miss or an empty slot needs only pid)
                 pid = slot_pid(wf, g, i);
@@ -602,9 +588,6 @@ __global__ void __launch_bounds__(BLOCK) wf_shade_slots(const KernelParams kp, c
                     c.shades++;
                     o = xyz(o4);
                     d = xyz(d4);
-#if MCPT_WF_HIT_ID
-                    tri_hit_params(o, d, tris[htri], tris[htri + 1], tris[htri + 2], h.x, h.y, h.z);
-#endif
                     if (qe) scatter<true>(gm, sc.normals, htri, h.y, h.z, h.x, 0, sd, color, o, d);
                     else scatter<false>(gm, sc.normals, htri, h.y, h.z, h.x, kp.fresnel_kd, sd, color, o, d);
                     cont = true;
