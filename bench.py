@@ -436,7 +436,9 @@ def main():
                 roof.update(achieved=round(gbs, 2), frac=round(gbs / HBM_PEAK_GBS, 5), traffic=round(tot_b, 3),
                             traffic_unit="GB of HBM read+write per frame (all wavefront kernels)", kernels=kh,
                             kernels_note="per-kernel ms / GBps from the PMC passes, which run kernels one at a "
-                                         "time; the timed frame overlaps them on several streams")
+                                         "time; the timed frame overlaps them on several streams; frac_of_copy "
+                                         "can exceed 1 for read-mostly kernels (accumulate): the copy reference "
+                                         "moves equal read and write bytes")
                 ext = kh.get("extend", {})
                 vb = valu_block(ext.pop("valu_counters", {}), torch.cuda.get_device_properties(dev).multi_processor_count,
                                 ext.get("ms", 0.0), per_launch["rays"])
