@@ -8,7 +8,8 @@ statistical pin against the reference's own 1000-spp render.
   single-GPU image bit for bit; a second render is bit-identical (determinism);
   the image is finite and the light is the brightest region.
 * the same frame through the wavefront pipeline: bit-identical image, equal
-  counters; and C5 (4096 spp) likewise, twice (determinism).
+  counters; and C5 (4096 spp) likewise, twice (determinism); its 2 and 8
+  packed shards (one rank's work in bench.py's N-GPU runs) reassemble it.
 * RenderScene's progressive loop (10 launches x 100 spp, prevCount running
   mean, CUTracer.cu:378-398) at 800x600 with the published-render variant
   (luminance 30, untinted Fresnel) matches CV/result1.png statistically.
@@ -48,6 +49,31 @@ def test_fullsize_shards_and_determinism(mcpt, scene01):
     got = torch.full((H * W, 4), -1.0, dtype=torch.float32, device="cuda")
     for r in range(N):
         ps = mcpt.RenderParams(width=W, height=H, spp=1024, spp_chunk=32, shard_count=N, shard_index=r)
+        part = torch.zeros((ps.output_pixels(), 4), dtype=torch.float32, device="cuda")
+        scene01.render_device(ps, part.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        xy = torch.from_numpy(ps.shard_pixels().astype(np.int64)).cuda()
+        ok = xy[:, 0] >= 0
+        got[(xy[:, 1] * W + xy[:, 0])[ok]] = part[ok]
+    torch.cuda.synchronize()
+    scene01.stats()
+    assert torch.equal(got[:, :3], full[:, :3])
+
+
+@pytest.mark.parametrize("N", [2, 8])
+def test_fullsize_wavefront_shards_reassemble(mcpt, scene01, N):
+    """What one rank of bench.py's N-GPU run renders (the wavefront, packed
+    interleaved tiles, default batches = work / streams, implicit queue 0 with
+    the shard's pixel mapping): the N shards reassemble the whole-frame image
+    bit for bit."""
+    import torch
+    W = H = 1024
+    p = mcpt.RenderParams(width=W, height=H, spp=1024, spp_chunk=32, pipeline="wavefront")
+    full = torch.zeros((H * W, 4), dtype=torch.float32, device="cuda")
+    scene01.render_device(p, full.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    got = torch.full((H * W, 4), -1.0, dtype=torch.float32, device="cuda")
+    for r in range(N):
+        ps = mcpt.RenderParams(width=W, height=H, spp=1024, spp_chunk=32, shard_count=N, shard_index=r,
+                               packed=True, tile=8, pipeline="wavefront")
         part = torch.zeros((ps.output_pixels(), 4), dtype=torch.float32, device="cuda")
         scene01.render_device(ps, part.data_ptr(), torch.cuda.current_stream().cuda_stream)
         xy = torch.from_numpy(ps.shard_pixels().astype(np.int64)).cuda()
