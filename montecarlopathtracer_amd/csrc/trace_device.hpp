@@ -189,6 +189,19 @@ __device__ __forceinline__ void tri_accept(RayState& r, const TriDets& q, uint32
         r.hgamma = gamma;
     }
 }
+// (t, beta, gamma) of ray (o, d) against the triangle record A0..A2: the same
+// operations as the traversal's accepted hit, so a hit recomputed from the
+// triangle id is bit-identical to the one the traversal found
+__device__ __forceinline__ void tri_hit_params(V3 o, V3 d, const float4 A0, const float4 A1, const float4 A2,
+                                               float& t, float& beta, float& gamma) {
+    RayState r;
+    r.o = o;
+    r.d = d;
+    r.best = 0.0f;
+    TriDets q;
+    (void)tri_prefilter(r, A0, A1, A2, q);
+    tri_quotients(q, beta, gamma, t);
+}
 __device__ __forceinline__ void test_tri_v(RayState& r, const float4 A0, const float4 A1, const float4 A2, uint32_t k) {
     TriDets q;
     if (tri_prefilter(r, A0, A1, A2, q)) tri_accept(r, q, __float_as_uint(A0.w), k);

@@ -152,6 +152,16 @@ __device__ __forceinline__ uint32_t slot_pid(const WfParams& wf, uint32_t g, uin
 __device__ __forceinline__ bool implicit0(const KernelParams& kp, const WfParams& wf) {
     return MCPT_WF_IMPLICIT0 && !wf.sort && kp.mode != kModeQE;
 }
+// MCPT_WF_HIT_ID = 1 (default, queue order): extend writes only the hit
+// triangle's id (4 B, the first quarter of the hit stream as i32) and shade
+// recomputes t, beta, gamma of a scattering ray from it (tri_hit_params: the
+// traversal's own operations, bit-identical).  The 16-B hit records cost the
+// extend 2.4x their bytes in partly written L2 lines; C2 wavefront +3.7%
+// (12.70 -> 13.18, three rounds), C4 +2.8%.
+#ifndef MCPT_WF_HIT_ID
+#define MCPT_WF_HIT_ID 1
+#endif
+static_assert(MCPT_WF_SOA || !MCPT_WF_HIT_ID, "hit ids use the SoA hit stream");
 
 // ---- generate: primary rays of the batch (CUTracer.cu:186-211) -------------
 // Paths go to segments in groups of 2^group_shift (64 = one 8x8 tile of one
@@ -383,7 +393,9 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
             } else {
                 mode = kDead;
             }
-            if constexpr ((MCPT_WF_NT & 4) != 0 || (!IN_LDS && MCPT_WF_NT_HIT_GLOBAL))
+            if constexpr (MCPT_WF_HIT_ID && !SORT)   // (r holds the next ray by now: the id from hrec)
+                reinterpret_cast<int32_t*>(qb + qf(0, 2, qs))[seg0 + fslot] = __float_as_int(hrec.w);
+            else if constexpr ((MCPT_WF_NT & 4) != 0 || (!IN_LDS && MCPT_WF_NT_HIT_GLOBAL))
                 stq_nt(&qb[qf(seg0 + fslot, 2, qs)], hrec);
             else
                 qb[qf(seg0 + fslot, 2, qs)] = hrec;
@@ -538,8 +550,13 @@ __global__ void __launch_bounds__(BLOCK) wf_shade_slots(const KernelParams kp, c
         V3 o = v3(0, 0, 0), d = v3(0, 0, 0), color = v3(0, 0, 0);
         if (i < total) {
             const size_t js = seg0 + i;
+#if MCPT_WF_HIT_ID
+            const int32_t htri = reinterpret_cast<const int32_t*>(qb + qf(0, 2, qs))[js];
+            float4 h = make_float4(0, 0, 0, 0);
+#else
             const float4 h = ldq(&qb[qf(js, 2, qs)]);
             const int32_t htri = __float_as_int(h.w);
+#endif
             float4 o4, d4, ps;
             if (imp) {   // generate's primary ray, recomputed (a miss or an empty slot needs only pid)
                 pid = slot_pid(wf, g, i);
@@ -588,6 +605,9 @@ __global__ void __launch_bounds__(BLOCK) wf_shade_slots(const KernelParams kp, c
                     c.shades++;
                     o = xyz(o4);
                     d = xyz(d4);
+#if MCPT_WF_HIT_ID
+                    tri_hit_params(o, d, tris[htri], tris[htri + 1], tris[htri + 2], h.x, h.y, h.z);
+#endif
                     if (qe) scatter<true>(gm, sc.normals, htri, h.y, h.z, h.x, 0, sd, color, o, d);
                     else scatter<false>(gm, sc.normals, htri, h.y, h.z, h.x, kp.fresnel_kd, sd, color, o, d);
                     cont = true;
@@ -679,7 +699,7 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams* wf_in, co
     // batch's shade and the tail of its extend overlap another batch's extend.
     // The shade then runs in workgroups that fit on a CU beside the extend's 16
     // waves (extend <= 88 VGPRs per lane, so 160 of the SIMD's 512 are left:
-    // two 64-VGPR shade waves; 4 B of LDS): 512 threads for LDS scenes (one
+    // two <= 80-VGPR shade waves; 4 B of LDS): 512 threads for LDS scenes (one
     // 1024-thread extend workgroup with 157 KB of LDS per CU), 256 for global
     // scenes (four 256-thread extend workgroups), so shading fills the
     // extend's idle issue slots instead of waiting for it (C2 wavefront 10.10
