@@ -358,18 +358,23 @@ struct Plan {
     mcpt::KernelParams kp;
     size_t out_pixels;
     int pipeline;
+    int wf_streams;              // wavefront streams (wavefront_streams)
     uint32_t wf_capacity;        // paths per wavefront batch
     int32_t wf_sort;             // wavefront material sort (mcpt_render_params::wf_sort)
 };
 
-// wavefront streams: 2 for scenes in LDS, 4 for scenes in global memory (C2
+// wavefront streams: 2-3 for scenes in LDS, 4 for scenes in global memory (C2
 // 1024 spp, streams x batch: 2 x 2^27 11.48, 2 x 2^26 11.46, 4 x 2^27 11.52,
 // 4 x 2^26 10.93; C4 1024 spp: 1 x 2^28 6.14, 2 x 2^28 8.07, 3 x 2^27 8.17,
 // 4 x 2^27 8.28 G rays/s, means of 2-3 runs).  MCPT_WF_STREAMS=n (1..4)
 // overrides; 1 = every batch on the caller's stream.
-int wavefront_streams(const mcpt_scene& s) {
+// LDS scenes: 3 streams for frames of >= 2^29 paths (C2 after the id-only hit
+// records: 2 x 2^28 13.48 / 13.45, 3 x 2^27 13.65 / 13.56, 3 x 2^30/9 13.65 /
+// 13.59 G rays/s), 2 below (one rank's C2 share at N = 8, 2^27 paths: 35.4 ms
+// on 2 streams, 37.6 on 3)
+int wavefront_streams(const mcpt_scene& s, uint64_t work) {
     const char* e = std::getenv("MCPT_WF_STREAMS");
-    const int n = e ? std::atoi(e) : (s.gpu.node_boxes ? 4 : 2);
+    const int n = e ? std::atoi(e) : (s.gpu.node_boxes ? 4 : (work >= (uint64_t(1) << 29) ? 3 : 2));
     return n < 1 ? 1 : (n > mcpt::kMaxWfStreams ? mcpt::kMaxWfStreams : n);
 }
 
@@ -462,10 +467,11 @@ Plan make_plan(const mcpt_scene& s, const mcpt_render_params* p) {
         // rays/s.  Global-memory scenes on 4 streams: 2^27 each (see wavefront_streams);
         // LDS scenes on 2 streams: 2^28 each (C2 2 x 2^27 12.90, 2 x 2^28 13.03,
         // 3 x 2^27 13.06, 4 x 2^27 12.55 G rays/s, two rounds each; 86 GB of queues)
-        const int nstr = wavefront_streams(s);
-        const bool big = !s.gpu.node_boxes || nstr == 1;
-        uint64_t cap = p->wf_batch ? p->wf_batch : (big ? (1u << 28) : (1u << 27));
         const uint64_t work = std::max<uint64_t>(npix, 1) * std::max<uint64_t>(p->spp, chunk);
+        const int nstr = wavefront_streams(s, work);
+        pl.wf_streams = nstr;
+        const bool big = nstr == 1 || (!s.gpu.node_boxes && nstr == 2);
+        uint64_t cap = p->wf_batch ? p->wf_batch : (big ? (1u << 28) : (1u << 27));
         // a default batch gives every stream a batch of its own (one rank's C2
         // share at 8 GPUs, 2^27 paths: one 2^27 batch 9.26, two 2^26 12.61, four
         // 2^25 12.13 G rays/s; the megakernel 11.22)
@@ -579,7 +585,7 @@ void render_async(mcpt_scene& s, const mcpt_render_params* p, float* d_fb, hipSt
     Plan pl = make_plan(s, p);
     pl.kp.raw_mean = raw_mean ? 1 : 0;
     // the tail split hands units out by sample, so per-unit counters need whole units
-    const int wf_sets = pl.pipeline == MCPT_PIPELINE_WAVEFRONT ? wavefront_streams(s) : 1;
+    const int wf_sets = pl.pipeline == MCPT_PIPELINE_WAVEFRONT ? pl.wf_streams : 1;
     prepare_workspace(s, pl.kp, pl.pipeline == MCPT_PIPELINE_MEGAKERNEL && !d_unit_counters, wf_sets);
     pl.kp.unit_counters = d_unit_counters;
     Timing t;
@@ -1163,7 +1169,7 @@ int mcpt_scene_reserve(mcpt_scene* s, const mcpt_render_params* p) {
         auto reserve = [&](mcpt_scene& sc, const mcpt_render_params* q) {
             set_device(sc);
             Plan pl = make_plan(sc, q);
-            const int sets = pl.pipeline == MCPT_PIPELINE_WAVEFRONT ? wavefront_streams(sc) : 1;
+            const int sets = pl.pipeline == MCPT_PIPELINE_WAVEFRONT ? pl.wf_streams : 1;
             prepare_workspace(sc, pl.kp, pl.pipeline == MCPT_PIPELINE_MEGAKERNEL, sets);
             if (pl.pipeline == MCPT_PIPELINE_WAVEFRONT) {
                 mcpt::WfParams wf[mcpt::kMaxWfStreams];
