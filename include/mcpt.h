@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define MCPT_ABI_VERSION 5
+#define MCPT_ABI_VERSION 6
 
 enum {
     MCPT_OK = 0,
@@ -86,10 +86,11 @@ typedef struct {
     int32_t shard_index;
     int32_t packed;             /* 1: write owned tiles packed (tile-major) instead of row-major */
     int32_t pipeline;           /* MCPT_PIPELINE_*: megakernel (default) or wavefront; same image */
-    uint32_t wf_batch;          /* wavefront: max paths per batch (160 B of device memory each,
-                                   per stream: batches rotate over 2 streams for scenes in LDS,
-                                   4 for scenes in global memory; MCPT_WF_STREAMS overrides),
-                                   0 = 1<<27 (1<<28 for a global-memory scene on one stream) */
+    uint32_t wf_batch;          /* wavefront: max paths per batch and stream (160 B of device memory
+                                   each), 0 = automatic: LDS scenes 2^28 on one or two streams,
+                                   2^27 on three or more; global-memory scenes 2^28 on one stream,
+                                   2^27 on more; a default batch is also capped at work / streams
+                                   and shrunk (halved) until the queues fit wf_mem_limit */
     int32_t mode;               /* MCPT_MODE_*: path semantics (default CVMCTracer)       */
     int32_t lean;               /* 1: the megakernel counts only rays (paths, shades, spills,
                                    inner/leaf visits, leaf refs, triangle tests read 0; image and
@@ -102,6 +103,29 @@ typedef struct {
                                    its material's list, shade runs one material per wave over
                                    the lists); 0 (default) = shade in queue order (dense reads,
                                    faster); same image */
+    /* Scheduling.  None of these changes the image or the counters, only the
+     * time; 0 = automatic (the measured defaults).
+     * mcpt_plan_query reports the values a render would use. */
+    int32_t wf_streams;         /* wavefront HIP streams 1..4 the batches rotate over; 0: scenes in
+                                   LDS 2 (3 for frames of >= 2^29 paths), global-memory scenes 4 */
+    int32_t wf_refill;          /* wavefront extend: ready lanes before a wave refills (1..64);
+                                   0: 16 (LDS scenes), 8 (global-memory scenes) */
+    int32_t wf_group_shift;     /* wavefront, global-memory scenes: paths are dealt to queue
+                                   segments in groups of 2^k (6..14); 0: 14 */
+    int32_t ready_thresh;       /* megakernel: ready lanes before a shading round (1..64);
+                                   0: 32 (LDS scenes), 40 (global-memory scenes) */
+    int32_t tail_units_per_lane;/* megakernel tail split: the last units per lane handed out one
+                                   sample at a time; 0: 4; < 0: no tail split */
+    int32_t tail_units;         /* megakernel: exact number of tail-split units (overrides
+                                   tail_units_per_lane when > 0) */
+    uint64_t wf_mem_limit;      /* wavefront queue memory per render, bytes; 0: 90% of the device's
+                                   free memory (plus what this scene already holds).  A default
+                                   batch shrinks to fit; an explicit wf_batch that does not fit
+                                   fails with MCPT_E_NOMEM */
+    int32_t force_peer_copy;    /* multi-device renders: gather every shard with hipMemcpyPeerAsync,
+                                   also between replicas on one device (exercises the cross-device
+                                   path on a one-GPU box); 0: peer copies between devices only */
+    int32_t reserved_;          /* 0 */
 } mcpt_render_params;
 
 enum {
@@ -138,6 +162,37 @@ typedef struct {
                                    kernel_ms / reduce_ms are the slowest device's */
 } mcpt_render_stats;
 
+/* What a render with given params would run (mcpt_plan_query): the automatic
+ * scheduling choices resolved, and the device memory it needs. */
+typedef struct {
+    int32_t pipeline;           /* MCPT_PIPELINE_* */
+    int32_t variant;            /* kernel variant (as mcpt_render_stats::variant) */
+    int32_t wf_streams;         /* wavefront streams */
+    uint32_t wf_batch;          /* wavefront paths per batch and stream */
+    int32_t wf_refill;
+    int32_t wf_group_shift;     /* 6 for scenes in LDS (one 8x8 tile per group) */
+    int32_t ready_thresh;       /* megakernel */
+    int32_t tail_units;         /* megakernel tail-split units */
+    uint64_t work_paths;        /* paths of the render (this device's shard) */
+    uint64_t workspace_bytes;   /* device memory the render's workspace needs */
+    uint64_t wf_queue_bytes;    /* of which the wavefront's queues (what wf_mem_limit bounds) */
+    uint64_t device_free_bytes; /* free memory of the scene's device now */
+    int32_t devices;            /* devices the render runs on */
+    int32_t peer_access;        /* multi-device: 1 if peer access between every pair is enabled */
+} mcpt_plan_info;
+
+/* Scene creation options (mcpt_scene_create_ex). */
+typedef struct {
+    const char* kd_cache_dir;   /* on-disk KD-build cache directory (must exist); NULL = none */
+    int32_t host_only;          /* 1: no device allocation */
+    int32_t layout;             /* MCPT_LAYOUT_*: scene image placement */
+} mcpt_scene_options;
+
+enum {
+    MCPT_LAYOUT_AUTO = 0,       /* LDS image (8-B nodes) when it fits, else global memory with child boxes */
+    MCPT_LAYOUT_GLOBAL = 1      /* global memory with 48-B child-box pair records, whatever the size */
+};
+
 /* ---- library ------------------------------------------------------------ */
 int mcpt_abi_version(void);
 const char* mcpt_last_error(void);
@@ -155,7 +210,8 @@ int mcpt_device_count(int32_t* out);
 /* fill defaults = the CVMCTracer constants for scene 1 (CUTracer.cu:347-360) */
 void mcpt_render_params_default(mcpt_render_params* p);
 /* QuinEngine viewer defaults (GraphicsRTX.cpp:163-193, rtx.hlsl:373-404):
- * mode QE, 800x600, 1 spp per frame, depth 5, fovY 45, eye (0,5,17)        */
+ * mode QE, 640x480 (the QE window, QE/Main.cpp:11), 1 spp per frame, depth 5,
+ * fovY 45, eye (0,5,17)                                                       */
 void mcpt_render_params_quinengine(mcpt_render_params* p);
 
 /* ---- host model (ObjModel) ---------------------------------------------- */
@@ -198,6 +254,9 @@ int mcpt_scene_create_host(const mcpt_model* m, mcpt_scene** out);
  * QuinEngine/RTX/ShaderResource.hpp:128-179.)                              */
 int mcpt_scene_create_cached(const mcpt_model* m, const char* kd_cache_dir, int32_t host_only,
                              mcpt_scene** out, int32_t* cache_hit);
+/* General form of the three above (options may be NULL = defaults). */
+int mcpt_scene_create_ex(const mcpt_model* m, const mcpt_scene_options* options, mcpt_scene** out,
+                         int32_t* cache_hit);
 void mcpt_scene_destroy(mcpt_scene* s);
 int mcpt_scene_get_info(const mcpt_scene* s, mcpt_scene_info* out);
 /* KD tree as built (BFS order, QuinEngine/RTX/ShaderResource.hpp:128-179):
@@ -241,6 +300,8 @@ int mcpt_intersect(mcpt_scene* s, int64_t n, const float* o, const float* d, flo
  * per sample of the last ~4 units per lane) and the stack spill area (32 x
  * 16 B per lane); wavefront: 160 B per path of the batch.                    */
 int mcpt_scene_reserve(mcpt_scene* s, const mcpt_render_params* p);
+/* The scheduling a render of p would use and its memory (no allocation, no launch). */
+int mcpt_plan_query(mcpt_scene* s, const mcpt_render_params* p, mcpt_plan_info* out);
 
 #ifdef __cplusplus
 }

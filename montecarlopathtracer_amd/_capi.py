@@ -21,7 +21,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MCPT_LIB_PATH") or os.path.join(_HERE, "lib", "libmcpt.so")
 
 MCPT_OK = 0
-ABI_VERSION = 5
+ABI_VERSION = 6
 MODE_CVMCTRACER = 0
 MODE_QUINENGINE = 1
 PIPELINE_MEGAKERNEL = 0
@@ -56,6 +56,9 @@ class RenderParamsC(C.Structure):
         ("tile", C.c_int32), ("shard_count", C.c_int32), ("shard_index", C.c_int32), ("packed", C.c_int32),
         ("pipeline", C.c_int32), ("wf_batch", C.c_uint32), ("mode", C.c_int32), ("lean", C.c_int32),
         ("wf_sort", C.c_int32),
+        ("wf_streams", C.c_int32), ("wf_refill", C.c_int32), ("wf_group_shift", C.c_int32),
+        ("ready_thresh", C.c_int32), ("tail_units_per_lane", C.c_int32), ("tail_units", C.c_int32),
+        ("wf_mem_limit", C.c_uint64), ("force_peer_copy", C.c_int32), ("reserved_", C.c_int32),
     ]
 
 
@@ -68,6 +71,24 @@ class RenderStats(C.Structure):
     def as_dict(self):
         return {n: (getattr(self, n) if isinstance(getattr(self, n), float) else int(getattr(self, n)))
                 for n, _ in self._fields_}
+
+
+class PlanInfo(C.Structure):
+    _fields_ = [("pipeline", C.c_int32), ("variant", C.c_int32), ("wf_streams", C.c_int32), ("wf_batch", C.c_uint32),
+                ("wf_refill", C.c_int32), ("wf_group_shift", C.c_int32), ("ready_thresh", C.c_int32),
+                ("tail_units", C.c_int32), ("work_paths", C.c_uint64), ("workspace_bytes", C.c_uint64), ("wf_queue_bytes", C.c_uint64),
+                ("device_free_bytes", C.c_uint64), ("devices", C.c_int32), ("peer_access", C.c_int32)]
+
+    def as_dict(self):
+        return {n: int(getattr(self, n)) for n, _ in self._fields_}
+
+
+class SceneOptions(C.Structure):
+    _fields_ = [("kd_cache_dir", C.c_char_p), ("host_only", C.c_int32), ("layout", C.c_int32)]
+
+
+LAYOUT_AUTO = 0
+LAYOUT_GLOBAL = 1
 
 
 class ModelDesc(C.Structure):
@@ -102,6 +123,7 @@ _SIGS = {
     "mcpt_scene_create": (C.c_int, [_vp, C.POINTER(_vp)]),
     "mcpt_scene_create_host": (C.c_int, [_vp, C.POINTER(_vp)]),
     "mcpt_scene_create_cached": (C.c_int, [_vp, C.c_char_p, C.c_int32, C.POINTER(_vp), C.POINTER(C.c_int32)]),
+    "mcpt_scene_create_ex": (C.c_int, [_vp, C.POINTER(SceneOptions), C.POINTER(_vp), C.POINTER(C.c_int32)]),
     "mcpt_scene_destroy": (None, [_vp]),
     "mcpt_scene_get_info": (C.c_int, [_vp, C.POINTER(SceneInfo)]),
     "mcpt_scene_copy_kd": (C.c_int, [_vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_int32),
@@ -116,6 +138,7 @@ _SIGS = {
     "mcpt_shard_pixel_count": (C.c_int64, [C.POINTER(RenderParamsC)]),
     "mcpt_shard_pixels": (C.c_int, [C.POINTER(RenderParamsC), C.POINTER(C.c_int32)]),
     "mcpt_scene_reserve": (C.c_int, [_vp, C.POINTER(RenderParamsC)]),
+    "mcpt_plan_query": (C.c_int, [_vp, C.POINTER(RenderParamsC), C.POINTER(PlanInfo)]),
 }
 
 _lib = None

@@ -32,6 +32,8 @@ thread_local std::string g_err;
 // mcpt_init's device list for scenes created later on this thread (empty: the
 // current device only)
 thread_local std::vector<int> g_devices;
+// peer access enabled between every pair of distinct devices of g_devices
+thread_local bool g_peer_ok = true;
 
 int fail(int code, const std::string& msg) {
     g_err = msg;
@@ -42,7 +44,8 @@ int fail(int code, const std::string& msg) {
     do {                                                                                \
         hipError_t e_ = (expr);                                                         \
         if (e_ != hipSuccess)                                                           \
-            throw mcpt::Error{MCPT_E_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)}; \
+            throw mcpt::Error{e_ == hipErrorOutOfMemory ? MCPT_E_NOMEM : MCPT_E_DEVICE,   \
+                              std::string(#expr) + ": " + hipGetErrorString(e_)};       \
     } while (0)
 
 template <typename F>
@@ -97,6 +100,15 @@ struct Timing {
     hipEvent_t e[3];
 };
 
+// Restores the calling thread's current HIP device on every exit path
+struct DeviceGuard {
+    int prev = -1;
+    DeviceGuard() { (void)hipGetDevice(&prev); }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
 }  // namespace
 
 struct mcpt_scene {
@@ -127,6 +139,7 @@ struct mcpt_scene {
     // back into the caller's stream (created on first use)
     hipStream_t wf_stream[mcpt::kMaxWfStreams] = {};   // [0] unused (the caller's)
     hipEvent_t wf_fork = nullptr, wf_join[mcpt::kMaxWfStreams] = {};
+    bool peer_access = true;            // multi-device: peer access enabled between every device pair
 
     ~mcpt_scene() {
         if (!on_device) return;
@@ -223,7 +236,7 @@ DeviceOrder device_order(const mcpt::HostScene& hs) {
     return d;
 }
 
-void build_image(mcpt_scene& s) {
+void build_image(mcpt_scene& s, bool force_global) {
     const mcpt::HostScene& hs = s.hs;
     const uint32_t nt = static_cast<uint32_t>(hs.kd_tris.size());
     const uint32_t nn = static_cast<uint32_t>(hs.nodes.size());
@@ -256,7 +269,7 @@ void build_image(mcpt_scene& s) {
     size_t off_nodes, off_leafs, off_geoms;
     size_t total = image_size(ord, off_nodes, off_leafs, off_geoms);
     if (mcpt::lds_bytes_in_lds(static_cast<uint32_t>(std::min<size_t>(total, 0xFFFFFFF0u)), 4) + 32 > mcpt::kMaxLds ||
-        std::getenv("MCPT_EXP_GLOBAL")) {
+        force_global) {
         boxes = true;
         total = image_size(ord, off_nodes, off_leafs, off_geoms);
     }
@@ -360,22 +373,51 @@ struct Plan {
     int pipeline;
     int wf_streams;              // wavefront streams (wavefront_streams)
     uint32_t wf_capacity;        // paths per wavefront batch
+    bool wf_batch_explicit;      // the caller asked for this batch (not shrunk to fit memory)
     int32_t wf_sort;             // wavefront material sort (mcpt_render_params::wf_sort)
+    int32_t wf_refill;           // idle lanes before an extend wave refills
+    uint32_t wf_group_shift;     // global-memory scenes: paths dealt to segments in groups of 2^k
+    int64_t tail_per_lane;       // megakernel tail split: units per lane (< 0 off)
+    int64_t tail_exact;          // megakernel tail split: exact units (> 0 overrides)
+    uint64_t wf_mem_limit;       // mcpt_render_params::wf_mem_limit
+    uint64_t work;               // paths of the render
 };
+
+int clamp_i(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
 // wavefront streams: 2-3 for scenes in LDS, 4 for scenes in global memory (C2
 // 1024 spp, streams x batch: 2 x 2^27 11.48, 2 x 2^26 11.46, 4 x 2^27 11.52,
 // 4 x 2^26 10.93; C4 1024 spp: 1 x 2^28 6.14, 2 x 2^28 8.07, 3 x 2^27 8.17,
-// 4 x 2^27 8.28 G rays/s, means of 2-3 runs).  MCPT_WF_STREAMS=n (1..4)
-// overrides; 1 = every batch on the caller's stream.
+// 4 x 2^27 8.28 G rays/s, means of 2-3 runs).  mcpt_render_params::wf_streams
+// (1..4) overrides; 1 = every batch on the caller's stream.
 // LDS scenes: 3 streams for frames of >= 2^29 paths (C2 after the id-only hit
 // records: 2 x 2^28 13.48 / 13.45, 3 x 2^27 13.65 / 13.56, 3 x 2^30/9 13.65 /
 // 13.59 G rays/s), 2 below (one rank's C2 share at N = 8, 2^27 paths: 35.4 ms
 // on 2 streams, 37.6 on 3)
-int wavefront_streams(const mcpt_scene& s, uint64_t work) {
-    const char* e = std::getenv("MCPT_WF_STREAMS");
-    const int n = e ? std::atoi(e) : (s.gpu.node_boxes ? 4 : (work >= (uint64_t(1) << 29) ? 3 : 2));
-    return n < 1 ? 1 : (n > mcpt::kMaxWfStreams ? mcpt::kMaxWfStreams : n);
+int wavefront_streams(const mcpt_scene& s, uint64_t work, const mcpt_render_params* p) {
+    const int n = p->wf_streams > 0 ? p->wf_streams
+                                    : (s.gpu.node_boxes ? 4 : (work >= (uint64_t(1) << 29) ? 3 : 2));
+    return clamp_i(n, 1, mcpt::kMaxWfStreams);
+}
+
+// Device memory of one stream's wavefront workspace for batches of `cap`
+// paths (prepare_wavefront carves it): two ray queues of four float4 streams,
+// radiance, four class lists (160 B per slot), per-bounce counters.  Segments
+// hold whole path groups (2^group_shift paths: 64 for LDS scenes, up to 2^14
+// for global-memory ones): up to one group of slots per segment beyond the paths.
+struct WfLayout {
+    size_t cap_slots, f4, need;
+};
+WfLayout wf_layout(const mcpt_scene& s, const Plan& pl, uint64_t cap) {
+    const mcpt::KernelParams& kp = pl.kp;
+    const size_t nseg = static_cast<size_t>(mcpt::wavefront_segments(s.gpu, s.cus));
+    const size_t queries = kp.mode == MCPT_MODE_QUINENGINE ? 3 * size_t(kp.max_depth) + 1 : size_t(kp.max_depth) + 1;
+    const size_t bounces = (queries + 1) * nseg;
+    WfLayout l;
+    l.cap_slots = size_t(cap) + (nseg << pl.wf_group_shift);
+    l.f4 = l.cap_slots * 16;
+    l.need = (2 * 4 * l.f4 + l.f4 + 4 * l.cap_slots * 4 + bounces * sizeof(mcpt::WfCounters) + 256 + 255) & ~size_t(255);
+    return l;
 }
 
 Plan make_plan(const mcpt_scene& s, const mcpt_render_params* p) {
@@ -383,6 +425,13 @@ Plan make_plan(const mcpt_scene& s, const mcpt_render_params* p) {
     if (p->width <= 0 || p->height <= 0) throw mcpt::Error{MCPT_E_INVALID, "width/height must be positive"};
     if (p->spp == 0) throw mcpt::Error{MCPT_E_INVALID, "spp must be > 0"};
     if (p->max_depth < 0 || p->max_depth > 1000) throw mcpt::Error{MCPT_E_INVALID, "max_depth out of range"};
+    if (p->wf_streams < 0 || p->wf_streams > mcpt::kMaxWfStreams)
+        throw mcpt::Error{MCPT_E_INVALID, "wf_streams must be 0 (automatic) or 1..4"};
+    if (p->wf_refill < 0 || p->wf_refill > 64 || p->ready_thresh < 0 || p->ready_thresh > 64)
+        throw mcpt::Error{MCPT_E_INVALID, "wf_refill / ready_thresh must be 0 (automatic) or 1..64"};
+    if (p->wf_group_shift != 0 && (p->wf_group_shift < 6 || p->wf_group_shift > 14))
+        throw mcpt::Error{MCPT_E_INVALID, "wf_group_shift must be 0 (automatic) or 6..14"};
+    if (p->tail_units < 0) throw mcpt::Error{MCPT_E_INVALID, "tail_units must be >= 0"};
     const int T = p->tile > 0 ? p->tile : 8;
     if (T > 256) throw mcpt::Error{MCPT_E_INVALID, "tile too large"};
     const int sc = p->shard_count > 1 ? p->shard_count : 1;
@@ -448,18 +497,26 @@ Plan make_plan(const mcpt_scene& s, const mcpt_render_params* p) {
     } else {
         k.key = tea16(static_cast<uint32_t>(p->seed), static_cast<uint32_t>(p->seed >> 32));
     }
-    {
-        // lanes ready before a shading round: scenes in LDS 32 (sweep 16..48);
-        // scenes in global memory 40 (C4: 24 5.15, 32 5.38, 40 5.50, 48 5.39 G rays/s)
-        const char* e = std::getenv("MCPT_READY_THRESH");
-        const int th = e ? std::atoi(e) : (s.gpu.node_boxes == 1 ? 40 : 32);
-        k.ready_thresh = th < 1 ? 1 : (th > 64 ? 64 : th);
-    }
+    // lanes ready before a shading round: scenes in LDS 32 (sweep 16..48);
+    // scenes in global memory 40 (C4: 24 5.15, 32 5.38, 40 5.50, 48 5.39 G rays/s)
+    k.ready_thresh = p->ready_thresh > 0 ? p->ready_thresh : (s.gpu.node_boxes == 1 ? 40 : 32);
     pl.out_pixels = k.packed ? size_t(npix) : size_t(p->width) * size_t(p->height);
     if (p->pipeline != MCPT_PIPELINE_MEGAKERNEL && p->pipeline != MCPT_PIPELINE_WAVEFRONT)
         throw mcpt::Error{MCPT_E_INVALID, "unknown pipeline"};
     pl.pipeline = p->pipeline;
     pl.wf_sort = p->wf_sort ? 1 : 0;
+    // idle lanes before an extend wave refills: 16 for scenes in LDS (C2 sweep
+    // 8 / 16 / 24: 10.08 / 10.28 / 10.19 G rays/s), 8 for scenes in global
+    // memory (C4 256 spp, 2..40: 6.18 / 6.20 (4-12) / 6.14 (16) / 5.79 (32) / 5.53)
+    pl.wf_refill = p->wf_refill > 0 ? p->wf_refill : (s.gpu.node_boxes ? 8 : 16);
+    // global-memory scenes keep whole image regions together per segment (C4
+    // sweep: 2^6 0.63, 2^8 0.47, 2^10 0.44, 2^12 0.62, contiguous 0.79 G rays/s)
+    pl.wf_group_shift = s.gpu.node_boxes ? static_cast<uint32_t>(p->wf_group_shift > 0 ? p->wf_group_shift : 14) : 6u;
+    // tail split: 4 units per lane (a whole frame +0.3% over 6; rank 0 of 8
+    // shards at 97.0% of ideal, 6: 96.5%, 8: 95.7%, 10: 94.8%)
+    pl.tail_per_lane = p->tail_units_per_lane == 0 ? 4 : p->tail_units_per_lane;
+    pl.tail_exact = p->tail_units;
+    pl.wf_mem_limit = p->wf_mem_limit;
     {
         // default batch: big (160 B of queues per path and stream; fewer launches,
         // shorter relative tails).  One stream: C2 2^24 5.59, 2^25 6.43, 2^26 7.07,
@@ -468,7 +525,8 @@ Plan make_plan(const mcpt_scene& s, const mcpt_render_params* p) {
         // LDS scenes on 2 streams: 2^28 each (C2 2 x 2^27 12.90, 2 x 2^28 13.03,
         // 3 x 2^27 13.06, 4 x 2^27 12.55 G rays/s, two rounds each; 86 GB of queues)
         const uint64_t work = std::max<uint64_t>(npix, 1) * std::max<uint64_t>(p->spp, chunk);
-        const int nstr = wavefront_streams(s, work);
+        pl.work = npix * p->spp;
+        const int nstr = wavefront_streams(s, work, p);
         pl.wf_streams = nstr;
         const bool big = nstr == 1 || (!s.gpu.node_boxes && nstr == 2);
         uint64_t cap = p->wf_batch ? p->wf_batch : (big ? (1u << 28) : (1u << 27));
@@ -480,17 +538,59 @@ Plan make_plan(const mcpt_scene& s, const mcpt_render_params* p) {
         cap = std::min<uint64_t>(cap, work);
         cap = std::min<uint64_t>(cap, uint64_t(1) << 28);               // u32 slot arithmetic; 160 B per path
         pl.wf_capacity = static_cast<uint32_t>(cap);
+        pl.wf_batch_explicit = p->wf_batch != 0;
     }
     return pl;
 }
 
-// tail_split: the megakernel hands the last MCPT_TAIL_UNITS_PER_LANE (default
-// 4) units per lane of the work-unit order out one sample at a time
+// Fit the wavefront's queues into device memory: the budget is
+// wf_mem_limit, or 90% of what the device has free plus what this scene's
+// workspace already holds.  A default batch is halved until every stream's
+// queues fit (never below one pixel's chunk); an explicit batch that does not
+// fit is an error, not a failed hipMalloc half-way through a render.
+void fit_wavefront(const mcpt_scene& s, Plan& pl) {
+    if (pl.pipeline != MCPT_PIPELINE_WAVEFRONT) return;
+    uint64_t budget = pl.wf_mem_limit;
+    if (!budget) {
+        size_t fr = 0, tot = 0;
+        HIP_TRY(hipMemGetInfo(&fr, &tot));
+        budget = static_cast<uint64_t>((static_cast<double>(fr) + static_cast<double>(s.ws.wf_bytes)) * 0.9);
+    }
+    auto need = [&](uint64_t cap) { return uint64_t(wf_layout(s, pl, cap).need) * uint64_t(pl.wf_streams); };
+    uint64_t cap = pl.wf_capacity;
+    if (!pl.wf_batch_explicit)
+        while (need(cap) > budget && cap / 2 >= pl.kp.chunk && cap > (uint64_t(1) << 16)) cap /= 2;
+    if (need(cap) > budget) {
+        char msg[256];
+        std::snprintf(msg, sizeof msg,
+                      "wavefront queues for batches of %llu paths need %.2f GB on %d stream(s); budget %.2f GB "
+                      "(wf_mem_limit or 90%% of free device memory): lower wf_batch / wf_streams",
+                      static_cast<unsigned long long>(cap), need(cap) / 1e9, pl.wf_streams, budget / 1e9);
+        throw mcpt::Error{MCPT_E_NOMEM, msg};
+    }
+    pl.wf_capacity = static_cast<uint32_t>(cap);
+}
+
+// tail_split: the megakernel hands the last Plan::tail_per_lane (default 4)
+// units per lane of the work-unit order out one sample at a time
 // (KernelParams::tail_units).  Without it a lane's last whole unit (32 samples,
 // ~3.5 ms) set the kernel's end: at 1024 spp, rank 0 of 8 ran 64.4 ms against
 // 55.5 ideal (86%); split 2 / 4 / 6 / 8 / 12 per lane: 92 / 96 / 98 / 97 / 96%,
 // 1-GPU frame unchanged (442 -> 440 ms at 6).
-void prepare_workspace(mcpt_scene& s, mcpt::KernelParams& k, bool tail_split = false, int spill_sets = 1) {
+uint64_t tail_units_for(const mcpt_scene& s, const Plan& pl) {
+    const mcpt::KernelParams& k = pl.kp;
+    if (k.chunk <= 1) return 0;
+    const uint64_t lanes = static_cast<uint64_t>(mcpt::total_lanes_for(s.gpu.image_bytes, s.cus));
+    uint64_t tail = pl.tail_exact > 0 ? static_cast<uint64_t>(pl.tail_exact)
+                                      : (pl.tail_per_lane > 0 ? static_cast<uint64_t>(pl.tail_per_lane) * lanes : 0);
+    tail = std::min<uint64_t>(tail, k.total_units);
+    // item indices and tail slots stay below 2^31
+    while (tail && uint64_t(k.total_units - tail) + tail * k.chunk >= (uint64_t(1) << 31)) tail >>= 1;
+    return tail;
+}
+
+void prepare_workspace(mcpt_scene& s, Plan& pl, bool tail_split = false, int spill_sets = 1) {
+    mcpt::KernelParams& k = pl.kp;
     ensure_buf(s.ws.partial, s.ws.partial_bytes, size_t(k.nchunks) * k.npix_local * 16);
     if (!s.ws.small) {
         HIP_TRY(hipMalloc(&s.ws.small, 256));
@@ -506,18 +606,8 @@ void prepare_workspace(mcpt_scene& s, mcpt::KernelParams& k, bool tail_split = f
     k.tail_units = k.total_units;
     k.total_items = k.total_units;
     k.tail_buf = nullptr;
-    if (tail_split && k.chunk > 1) {
-        // MCPT_TAIL_UNITS: exact count (tests); MCPT_TAIL_UNITS_PER_LANE: per lane
-        const char* e = std::getenv("MCPT_TAIL_UNITS_PER_LANE");
-        const char* ea = std::getenv("MCPT_TAIL_UNITS");
-        // 4 per lane: a whole frame +0.3% over 6; rank 0 of 8 shards at 97.0% of
-        // ideal (6: 96.5%, 8: 95.7%, 10: 94.8%) since the seed table and the
-        // faster traversal shortened the units
-        const uint64_t per = e ? static_cast<uint64_t>(std::max(0, std::atoi(e))) : 4;
-        uint64_t tail = ea ? static_cast<uint64_t>(std::max(0LL, std::atoll(ea))) : per * lanes;
-        tail = std::min<uint64_t>(tail, k.total_units);
-        // item indices and tail slots stay below 2^31
-        while (tail && uint64_t(k.total_units - tail) + tail * k.chunk >= (uint64_t(1) << 31)) tail >>= 1;
+    if (tail_split) {
+        const uint64_t tail = tail_units_for(s, pl);
         if (tail) {
             ensure_buf(s.ws.tail, s.ws.tail_bytes, size_t(tail) * k.chunk * 16);
             k.tail_units = k.total_units - static_cast<uint32_t>(tail);
@@ -530,34 +620,33 @@ void prepare_workspace(mcpt_scene& s, mcpt::KernelParams& k, bool tail_split = f
 // wavefront workspace: 2 ray queues (o, d float4), hits, 4 class lists,
 // path state and radiance, per-bounce counters -- carved from one buffer, once
 // per stream (`sets`: batches rotate over the wavefront's streams, each with its own)
-
 void prepare_wavefront(mcpt_scene& s, const Plan& pl, int sets, mcpt::WfParams* out) {
-    const size_t cap = pl.wf_capacity;
-    const size_t queries = pl.kp.mode == MCPT_MODE_QUINENGINE ? 3 * size_t(pl.kp.max_depth) + 1 : size_t(pl.kp.max_depth) + 1;
-    const size_t bounces = (queries + 1) * size_t(mcpt::wavefront_segments(s.gpu.image_bytes, s.cus));
-    // segments hold whole path groups (<= 2^14): up to nseg groups of slots beyond the paths
-    const size_t cap_slots = cap + size_t(mcpt::wavefront_segments(s.gpu.image_bytes, s.cus)) * 16384;
-    const size_t f4 = cap_slots * 16;
-    const size_t need = (2 * 4 * f4 + f4 + 4 * cap_slots * 4 + bounces * sizeof(mcpt::WfCounters) + 256 + 255) & ~size_t(255);
-    ensure_buf(s.ws.wf, s.ws.wf_bytes, need * size_t(sets));
-    const char* e = std::getenv("MCPT_WF_REFILL");
-    // idle lanes before an extend wave refills: 16 for scenes in LDS (C2 sweep
-    // 8 / 16 / 24: 10.08 / 10.28 / 10.19 G rays/s), 8 for scenes in global
-    // memory (C4 256 spp, 2..40: 6.18 / 6.20 (4-12) / 6.14 (16) / 5.79 (32) / 5.53)
-    const int th = e ? std::atoi(e) : (s.gpu.node_boxes ? 8 : 16);
+    const WfLayout l = wf_layout(s, pl, pl.wf_capacity);
+    ensure_buf(s.ws.wf, s.ws.wf_bytes, l.need * size_t(sets));
     for (int h = 0; h < sets; ++h) {
-        char* b = static_cast<char*>(s.ws.wf) + size_t(h) * need;
+        char* b = static_cast<char*>(s.ws.wf) + size_t(h) * l.need;
         mcpt::WfParams& w = out[h];
         std::memset(&w, 0, sizeof w);
-        w.q[0] = reinterpret_cast<float4*>(b); b += 4 * f4;
-        w.q[1] = reinterpret_cast<float4*>(b); b += 4 * f4;
-        w.radiance = reinterpret_cast<float4*>(b); b += f4;
-        w.cls_list = reinterpret_cast<uint32_t*>(b); b += 4 * cap_slots * 4;
+        w.q[0] = reinterpret_cast<float4*>(b); b += 4 * l.f4;
+        w.q[1] = reinterpret_cast<float4*>(b); b += 4 * l.f4;
+        w.radiance = reinterpret_cast<float4*>(b); b += l.f4;
+        w.cls_list = reinterpret_cast<uint32_t*>(b); b += 4 * l.cap_slots * 4;
         w.cnt = reinterpret_cast<mcpt::WfCounters*>(b);
-        w.capacity = static_cast<uint32_t>(cap);       // paths per batch (pid range)
-        w.slot_stride = static_cast<uint32_t>(cap_slots);
-        w.refill_thresh = th < 1 ? 1 : (th > 64 ? 64 : th);
+        w.capacity = pl.wf_capacity;                   // paths per batch (pid range)
+        w.slot_stride = static_cast<uint32_t>(l.cap_slots);
+        w.refill_thresh = clamp_i(pl.wf_refill, 1, 64);
+        w.group_shift = pl.wf_group_shift;
         w.sort = pl.wf_sort;
+    }
+}
+
+// the wavefront's side streams and their fork / join events (created once per
+// scene, outside any stream capture: mcpt_scene_reserve calls this too)
+void ensure_wf_streams(mcpt_scene& s, int n) {
+    if (n > 1 && !s.wf_fork) HIP_TRY(hipEventCreateWithFlags(&s.wf_fork, hipEventDisableTiming));
+    for (int i = 1; i < n; i++) {
+        if (!s.wf_stream[i]) HIP_TRY(hipStreamCreateWithFlags(&s.wf_stream[i], hipStreamNonBlocking));
+        if (!s.wf_join[i]) HIP_TRY(hipEventCreateWithFlags(&s.wf_join[i], hipEventDisableTiming));
     }
 }
 
@@ -583,10 +672,11 @@ void render_async(mcpt_scene& s, const mcpt_render_params* p, float* d_fb, hipSt
     }
     set_device(s);
     Plan pl = make_plan(s, p);
+    fit_wavefront(s, pl);
     pl.kp.raw_mean = raw_mean ? 1 : 0;
     // the tail split hands units out by sample, so per-unit counters need whole units
     const int wf_sets = pl.pipeline == MCPT_PIPELINE_WAVEFRONT ? pl.wf_streams : 1;
-    prepare_workspace(s, pl.kp, pl.pipeline == MCPT_PIPELINE_MEGAKERNEL && !d_unit_counters, wf_sets);
+    prepare_workspace(s, pl, pl.pipeline == MCPT_PIPELINE_MEGAKERNEL && !d_unit_counters, wf_sets);
     pl.kp.unit_counters = d_unit_counters;
     Timing t;
     if (!s.free_timing.empty()) {
@@ -602,13 +692,9 @@ void render_async(mcpt_scene& s, const mcpt_render_params* p, float* d_fb, hipSt
         mcpt::WfStreams wst{};
         wst.n = wf_sets;
         wst.st[0] = st;
-        if (wf_sets > 1 && !s.wf_fork) HIP_TRY(hipEventCreateWithFlags(&s.wf_fork, hipEventDisableTiming));
+        ensure_wf_streams(s, wf_sets);
         wst.fork = s.wf_fork;
         for (int i = 1; i < wf_sets; i++) {
-            if (!s.wf_stream[i]) {
-                HIP_TRY(hipStreamCreateWithFlags(&s.wf_stream[i], hipStreamNonBlocking));
-                HIP_TRY(hipEventCreateWithFlags(&s.wf_join[i], hipEventDisableTiming));
-            }
             wst.st[i] = s.wf_stream[i];
             wst.join[i] = s.wf_join[i];
         }
@@ -677,6 +763,7 @@ void read_stats(mcpt_scene& s, mcpt_render_stats* out) {
 // for bit.  Cross-device order: every shard waits for `start` (recorded on the
 // caller's stream), the caller's stream waits for every shard's `done`.
 void render_multi(mcpt_scene& s, const mcpt_render_params* p, float* d_fb, hipStream_t st) {
+    DeviceGuard guard;   // an error on a replica's device must not leave that device current
     set_device(s);
     const Plan full = make_plan(s, p);                  // validates p; row-major output
     const int n = 1 + static_cast<int>(s.replicas.size());
@@ -703,7 +790,7 @@ void render_multi(mcpt_scene& s, const mcpt_render_params* p, float* d_fb, hipSt
         HIP_TRY(hipStreamWaitEvent(R.stream, s.start, 0));
         render_async(R, &pr, static_cast<float*>(R.ws.fb), R.stream, nullptr, true);
         char* dst = static_cast<char*>(s.gather) + size_t(r) * slot * 16;
-        if (R.device == s.device)
+        if (R.device == s.device && !p->force_peer_copy)
             HIP_TRY(hipMemcpyAsync(dst, R.ws.fb, bytes, hipMemcpyDeviceToDevice, R.stream));
         else
             HIP_TRY(hipMemcpyPeerAsync(dst, s.device, R.ws.fb, R.device, bytes, R.stream));
@@ -767,13 +854,37 @@ const char* mcpt_last_error(void) { return g_err.c_str(); }
 int mcpt_init(const int32_t* devices, int32_t n) {
     return guarded([&]() -> int {
         if (n < 0 || (n > 0 && !devices)) return fail(MCPT_E_INVALID, "bad device list");
-        if (n == 0) return MCPT_OK;
+        if (n == 0) {                     // the current device, single-device scenes
+            g_devices.clear();
+            g_peer_ok = true;
+            return MCPT_OK;
+        }
         int count = 0;
         HIP_TRY(hipGetDeviceCount(&count));
         for (int i = 0; i < n; ++i)
             if (devices[i] < 0 || devices[i] >= count) return fail(MCPT_E_INVALID, "device ordinal out of range");
+        // peer access between every pair of distinct listed devices, so the
+        // multi-device gather's hipMemcpyPeerAsync is a direct xGMI DMA (without
+        // it the runtime stages the copy through host memory); "already
+        // enabled" is success, a pair without peer capability keeps the staged copy
+        bool peer_ok = true;
+        for (int i = 0; i < n; ++i)
+            for (int j = 0; j < n; ++j) {
+                if (devices[i] == devices[j]) continue;
+                int can = 0;
+                HIP_TRY(hipDeviceCanAccessPeer(&can, devices[i], devices[j]));
+                if (!can) {
+                    peer_ok = false;
+                    continue;
+                }
+                HIP_TRY(hipSetDevice(devices[i]));
+                const hipError_t e = hipDeviceEnablePeerAccess(devices[j], 0);
+                if (e == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+                else HIP_TRY(e);
+            }
         HIP_TRY(hipSetDevice(devices[0]));
         g_devices.assign(devices, devices + n);
+        g_peer_ok = peer_ok;
         return MCPT_OK;
     });
 }
@@ -792,7 +903,7 @@ void mcpt_render_params_quinengine(mcpt_render_params* p) {
     if (!p) return;
     mcpt_render_params_default(p);
     p->mode = MCPT_MODE_QUINENGINE;
-    p->width = 800; p->height = 600;                 // window size of the QE viewer
+    p->width = 640; p->height = 480;                 // the QE window (QE/Main.cpp:11, GraphicsRTX.hpp:34-35)
     p->spp = 1;                                       // one sample per pixel per frame (rtx.hlsl:373-404)
     p->max_depth = 5;                                 // sampleMC(..., 5) (rtx.hlsl:400)
     p->illum = 1.0f;                                  // no ILLUM factor
@@ -939,7 +1050,7 @@ int mcpt_model_group(const mcpt_model* m, int64_t g, char* name_buf, int64_t nam
 }
 
 static int scene_create_impl(const mcpt_model* m, mcpt_scene** out, bool device, const char* kd_cache_dir = nullptr,
-                             int32_t* cache_hit = nullptr) {
+                             int32_t* cache_hit = nullptr, int32_t layout = MCPT_LAYOUT_AUTO) {
     return guarded([&]() -> int {
         if (!m || !out) return fail(MCPT_E_INVALID, "NULL argument");
         auto s = std::make_unique<mcpt_scene>();
@@ -947,7 +1058,8 @@ static int scene_create_impl(const mcpt_model* m, mcpt_scene** out, bool device,
         mcpt::build_host_scene(m->m, s->hs, kd_cache_dir, &hit);
         if (cache_hit) *cache_hit = hit;
         if (s->hs.kd_tris.empty()) return fail(MCPT_E_INVALID, "scene has no triangles");
-        build_image(*s);
+        if (layout != MCPT_LAYOUT_AUTO && layout != MCPT_LAYOUT_GLOBAL) return fail(MCPT_E_INVALID, "unknown layout");
+        build_image(*s, layout == MCPT_LAYOUT_GLOBAL);
         if (device) {
             const size_t nt = s->hs.kd_tris.size();
             std::vector<float> nrm(nt * 12, 0.0f);
@@ -969,6 +1081,7 @@ static int scene_create_impl(const mcpt_model* m, mcpt_scene** out, bool device,
                 s->replicas.push_back(std::move(R));
             }
             HIP_TRY(hipSetDevice(devs[0]));
+            s->peer_access = g_peer_ok;
         }
         *out = s.release();
         return MCPT_OK;
@@ -980,6 +1093,12 @@ int mcpt_scene_create_host(const mcpt_model* m, mcpt_scene** out) { return scene
 int mcpt_scene_create_cached(const mcpt_model* m, const char* kd_cache_dir, int32_t host_only, mcpt_scene** out,
                              int32_t* cache_hit) {
     return scene_create_impl(m, out, host_only == 0, kd_cache_dir, cache_hit);
+}
+int mcpt_scene_create_ex(const mcpt_model* m, const mcpt_scene_options* o, mcpt_scene** out, int32_t* cache_hit) {
+    const mcpt_scene_options d{nullptr, 0, MCPT_LAYOUT_AUTO};
+    if (!o) o = &d;
+    const char* dir = o->kd_cache_dir && o->kd_cache_dir[0] ? o->kd_cache_dir : nullptr;
+    return scene_create_impl(m, out, o->host_only == 0, dir, cache_hit, o->layout);
 }
 
 void mcpt_scene_destroy(mcpt_scene* s) { delete s; }
@@ -1166,14 +1285,17 @@ int mcpt_shard_pixels(const mcpt_render_params* p, int32_t* xy) {
 int mcpt_scene_reserve(mcpt_scene* s, const mcpt_render_params* p) {
     return guarded([&]() -> int {
         if (!s || !s->on_device) return fail(MCPT_E_INVALID, "scene is not on a device");
+        DeviceGuard guard;
         auto reserve = [&](mcpt_scene& sc, const mcpt_render_params* q) {
             set_device(sc);
             Plan pl = make_plan(sc, q);
+            fit_wavefront(sc, pl);
             const int sets = pl.pipeline == MCPT_PIPELINE_WAVEFRONT ? pl.wf_streams : 1;
-            prepare_workspace(sc, pl.kp, pl.pipeline == MCPT_PIPELINE_MEGAKERNEL, sets);
+            prepare_workspace(sc, pl, pl.pipeline == MCPT_PIPELINE_MEGAKERNEL, sets);
             if (pl.pipeline == MCPT_PIPELINE_WAVEFRONT) {
                 mcpt::WfParams wf[mcpt::kMaxWfStreams];
                 prepare_wavefront(sc, pl, sets, wf);
+                ensure_wf_streams(sc, sets);   // streams and events exist before any capture
             }
         };
         if (!multi_device(*s, p, nullptr)) {
@@ -1194,6 +1316,55 @@ int mcpt_scene_reserve(mcpt_scene* s, const mcpt_render_params* p) {
         p0.shard_count = n; p0.shard_index = 0; p0.packed = 1;
         ensure_buf(s->gather, s->gather_bytes, size_t(n) * size_t(mcpt_shard_pixel_count(&p0)) * 16);
         if (!s->start) HIP_TRY(hipEventCreateWithFlags(&s->start, hipEventDisableTiming));
+        return MCPT_OK;
+    });
+}
+
+int mcpt_plan_query(mcpt_scene* s, const mcpt_render_params* p, mcpt_plan_info* out) {
+    return guarded([&]() -> int {
+        if (!s || !s->on_device || !out) return fail(MCPT_E_INVALID, "NULL argument or host-only scene");
+        DeviceGuard guard;
+        // a multi-device render: the plan of devices[0]'s shard (the largest)
+        mcpt_render_params q = *p;
+        const bool multi = multi_device(*s, p, nullptr);
+        if (multi) {
+            q.shard_count = 1 + static_cast<int32_t>(s->replicas.size());
+            q.shard_index = 0;
+            q.packed = 1;
+        }
+        set_device(*s);
+        Plan pl = make_plan(*s, &q);
+        fit_wavefront(*s, pl);
+        mcpt_plan_info r;
+        std::memset(&r, 0, sizeof r);
+        const uint32_t img = s->gpu.image_bytes;
+        const bool wf = pl.pipeline == MCPT_PIPELINE_WAVEFRONT;
+        r.pipeline = pl.pipeline;
+        if (wf) r.variant = (!s->gpu.node_boxes && mcpt::lds_bytes_in_lds(img, 4) + 32 <= mcpt::kMaxLds) ? 4 : 5;
+        else if (s->gpu.node_boxes) r.variant = 3;
+        else r.variant = mcpt::lds_bytes_in_lds(img, 8) <= mcpt::kMaxLds ? 1 : (mcpt::lds_bytes_in_lds(img, 4) <= mcpt::kMaxLds ? 2 : 3);
+        r.wf_streams = wf ? pl.wf_streams : 0;
+        r.wf_batch = wf ? pl.wf_capacity : 0;
+        r.wf_refill = wf ? pl.wf_refill : 0;
+        r.wf_group_shift = wf ? static_cast<int32_t>(pl.wf_group_shift) : 0;
+        r.ready_thresh = wf ? 0 : pl.kp.ready_thresh;
+        r.tail_units = wf ? 0 : static_cast<int32_t>(tail_units_for(*s, pl));
+        r.work_paths = pl.work;
+        const uint64_t lanes = static_cast<uint64_t>(mcpt::total_lanes_for(img, s->cus));
+        uint64_t ws = uint64_t(pl.kp.nchunks) * pl.kp.npix_local * 16 + 256 +
+                      uint64_t(wf ? pl.wf_streams : 1) * 32 * lanes * 16;
+        if (wf) {
+            r.wf_queue_bytes = uint64_t(wf_layout(*s, pl, pl.wf_capacity).need) * uint64_t(pl.wf_streams);
+            ws += r.wf_queue_bytes;
+        }
+        else ws += uint64_t(r.tail_units) * pl.kp.chunk * 16;
+        r.workspace_bytes = ws;
+        size_t fr = 0, tot = 0;
+        HIP_TRY(hipMemGetInfo(&fr, &tot));
+        r.device_free_bytes = fr;
+        r.devices = multi ? q.shard_count : 1;
+        r.peer_access = s->peer_access ? 1 : 0;
+        *out = r;
         return MCPT_OK;
     });
 }

@@ -165,6 +165,7 @@ struct WfParams {
     uint32_t nsc;                        // samples per chunk (ns = whole chunks of nsc)
     uint32_t nseg, seg;                  // segments (= extend workgroups) and slots per segment
     uint32_t group_shift;                // paths are dealt to segments in groups of 2^group_shift
+                                         // (the plan's for global-memory scenes; 6 in LDS)
     int32_t bounce;
     int32_t refill_thresh;               // idle lanes before an extend wave refills
     int32_t sort;                        // 1: material sort (class lists), 0: shade in queue order
@@ -183,7 +184,7 @@ void read_lane_use(unsigned long long out[6]);      // diagnostic build only: me
 void read_lane_use_wf(unsigned long long out[6]);   // wavefront extend
 #endif
 // wavefront queue segments (= extend workgroups) for a scene image
-int wavefront_segments(uint32_t image_bytes, int cus);
+int wavefront_segments(const GpuScene& sc, int cus);
 // wavefront pipeline: generate / extend / shade per bounce / accumulate per
 // batch, then the same reduction (events: ev0 before, ev1 after the batches)
 // wavefront streams: batch i runs on stream i mod n (st[0] = the caller's),

@@ -660,16 +660,9 @@ hipError_t launch_extend(const KernelParams& kp, const WfParams& wf, int grid, s
     return hipGetLastError();
 }
 
-bool wf_in_lds(uint32_t image_bytes) { return lds_bytes_in_lds(image_bytes, 4) + 32 <= kMaxLds; }
-
-// global-memory scenes keep whole image regions together per segment (C4
-// sweep: 2^6 0.63, 2^8 0.47, 2^10 0.44, 2^12 0.62, contiguous 0.79 G rays/s);
-// MCPT_WF_GROUP_SHIFT overrides for experiments
-uint32_t wf_global_group_shift() {
-    const char* e = std::getenv("MCPT_WF_GROUP_SHIFT");
-    const int v = e ? std::atoi(e) : 14;
-    return (uint32_t)(v < 6 ? 6 : (v > 14 ? 14 : v));
-}
+// the scene image (8-B node records) is copied into LDS; an image built with
+// child-box pair records (node_boxes) is always read from global memory
+bool wf_in_lds(const GpuScene& sc) { return !sc.node_boxes && lds_bytes_in_lds(sc.image_bytes, 4) + 32 <= kMaxLds; }
 
 }  // namespace
 
@@ -681,18 +674,16 @@ void read_lane_use_wf(unsigned long long out[6]) {   // wavefront extend lane-us
 }
 #endif
 
-int wavefront_segments(uint32_t image_bytes, int cus) {
-    return wf_in_lds(image_bytes) ? cus : cus * kGlobalBlocksPerCu;
-}
+int wavefront_segments(const GpuScene& sc, int cus) { return wf_in_lds(sc) ? cus : cus * kGlobalBlocksPerCu; }
 
 hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams* wf_in, const WfStreams& ws, int cus,
                             int max_bounces, hipEvent_t ev0, hipEvent_t ev1, hipEvent_t ev2, float4* fb,
                             int* variant_out) {
     KernelParams kp = kp_in;
     const uint32_t img = kp.scene.image_bytes;
-    const bool in_lds = wf_in_lds(img);
+    const bool in_lds = wf_in_lds(kp.scene);
     kp.total_lanes = (uint32_t)total_lanes_for(img, cus);
-    const uint32_t nseg = (uint32_t)wavefront_segments(img, cus);
+    const uint32_t nseg = (uint32_t)wavefront_segments(kp.scene, cus);
     const uint32_t per = in_lds ? 4u : 1u;                         // shade workgroups per segment
     // Several streams (ws.n > 1): batch i runs on stream i mod n, each stream
     // with its own queues/counters (wf_in[i]) and stack spill area, so one
@@ -713,8 +704,11 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams* wf_in, co
         for (int i = 1; i < ns; i++)
             if ((e = hipStreamWaitEvent(ws.st[i], ws.fork, 0)) != hipSuccess) return e;
     }
+    // Every launch error leaves the batch loops and still joins every forked
+    // stream back into the caller's stream below, so no side stream keeps
+    // writing the shared partial sums or spill areas behind a failed call.
     uint32_t batch = 0;
-    for (uint32_t chunk = 0; chunk < kp.nchunks;) {
+    for (uint32_t chunk = 0; chunk < kp.nchunks && e == hipSuccess;) {
         // whole-image batches may span several full chunks (fewer, longer launches)
         const uint32_t nsc = (kp.spp - chunk * kp.chunk) < kp.chunk ? (kp.spp - chunk * kp.chunk) : kp.chunk;
         uint32_t ncb = 1;
@@ -726,7 +720,7 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams* wf_in, co
         const uint32_t chunk0 = chunk;
         chunk += ncb;
         const uint32_t nb_max = wf_in[0].capacity / (ncb * nsc);
-        for (uint32_t v0 = 0; v0 < kp.npix_local; v0 += nb_max, ++batch) {
+        for (uint32_t v0 = 0; v0 < kp.npix_local && e == hipSuccess; v0 += nb_max, ++batch) {
             const int h = (int)(batch % (uint32_t)ns);
             const hipStream_t bs = ws.st[h];
             KernelParams kb = kp;
@@ -740,23 +734,25 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams* wf_in, co
             wf.v0 = v0;
             wf.nb = (kp.npix_local - v0) < nb_max ? (kp.npix_local - v0) : nb_max;
             const uint32_t n = wf.nb * wf.ns;
-            wf.group_shift = in_lds ? 6u : wf_global_group_shift();
+            // LDS scenes: one 8x8 tile of one sample per group; global-memory
+            // scenes: the planned group size (whole image regions per segment)
+            wf.group_shift = in_lds ? 6u : wf_in[h].group_shift;
             // whole groups per segment
             wf.seg = ((((n + (1u << wf.group_shift) - 1u) >> wf.group_shift) + nseg - 1) / nseg) << wf.group_shift;
             e = hipMemsetAsync(wf.cnt, 0, sizeof(WfCounters) * (size_t)nseg * (size_t)(max_bounces + 1), bs);
-            if (e != hipSuccess) return e;
+            if (e != hipSuccess) break;
             const uint32_t gen_grid = (n + kGenBlock - 1) / kGenBlock;
             hipLaunchKernelGGL(wf_generate, dim3(gen_grid < 16u * (uint32_t)cus ? gen_grid : 16u * (uint32_t)cus),
                                dim3(kGenBlock), 0, bs, kb, wf);
-            if ((e = hipGetLastError()) != hipSuccess) return e;
-            for (int b = 0; b < max_bounces; b++) {
+            if ((e = hipGetLastError()) != hipSuccess) break;
+            for (int b = 0; b < max_bounces && e == hipSuccess; b++) {
                 wf.bounce = b;
                 if (in_lds)
                     e = launch_extend<true, 4, kLdsBlock>(kb, wf, (int)nseg, lds_bytes_in_lds(img, 4) + 32, bs);
                 else
                     e = launch_extend<false, 8, kGlobalBlock>(kb, wf, (int)nseg, (size_t)8 * kGlobalBlock * 16 + 32,
                                                               bs);
-                if (e != hipSuccess) return e;
+                if (e != hipSuccess) break;
                 if (wf.sort)
                     hipLaunchKernelGGL(wf_shade, dim3(nseg * per), dim3(kShadeBlock), 0, bs, kb, wf, per);
                 else if (in_lds && ns == 1)   // alone on the GPU: 16 waves per segment keep HBM busy
@@ -765,16 +761,19 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams* wf_in, co
                     hipLaunchKernelGGL(wf_shade_slots<512>, dim3(nseg), dim3(512), 0, bs, kb, wf);
                 else
                     hipLaunchKernelGGL(wf_shade_slots<256>, dim3(nseg), dim3(256), 0, bs, kb, wf);
-                if ((e = hipGetLastError()) != hipSuccess) return e;
+                e = hipGetLastError();
             }
+            if (e != hipSuccess) break;
             hipLaunchKernelGGL(wf_accumulate, dim3((wf.nb + 255u) / 256u, ncb), dim3(256), 0, bs, kb, wf);
-            if ((e = hipGetLastError()) != hipSuccess) return e;
+            e = hipGetLastError();
         }
     }
-    for (int i = 1; i < ns; i++) {
-        if ((e = hipEventRecord(ws.join[i], ws.st[i])) != hipSuccess) return e;
-        if ((e = hipStreamWaitEvent(st, ws.join[i], 0)) != hipSuccess) return e;
+    for (int i = 1; i < ns; i++) {   // join (also after an error)
+        hipError_t j = hipEventRecord(ws.join[i], ws.st[i]);
+        if (j == hipSuccess) j = hipStreamWaitEvent(st, ws.join[i], 0);
+        if (e == hipSuccess) e = j;
     }
+    if (e != hipSuccess) return e;
     if (ev1 && (e = hipEventRecord(ev1, st)) != hipSuccess) return e;
     e = launch_reduce(kp, fb, st);
     if (e == hipSuccess && ev2) e = hipEventRecord(ev2, st);

@@ -174,6 +174,15 @@ class RenderParams:
     mode: str = "cvmctracer"          # or "quinengine": rtx.hlsl path semantics (see for_quinengine)
     lean: bool = False                # kernels without traversal counters (same image; bench timing)
     wf_sort: bool = False             # wavefront: material-sorted shade (class lists); same image
+    # scheduling (include/mcpt.h): never changes the image or the counters; 0 = automatic
+    wf_streams: int = 0               # wavefront HIP streams (1..4)
+    wf_refill: int = 0                # wavefront extend: ready lanes before a wave refills
+    wf_group_shift: int = 0           # wavefront, global-memory scenes: 2^k paths per segment group
+    ready_thresh: int = 0             # megakernel: ready lanes before a shading round
+    tail_units_per_lane: int = 0      # megakernel tail split per lane (< 0: off)
+    tail_units: int = 0               # megakernel: exact tail-split units (> 0 overrides)
+    wf_mem_limit: int = 0             # wavefront queue memory budget in bytes (0: 90% of free)
+    force_peer_copy: bool = False     # multi-device: hipMemcpyPeerAsync also between same-device replicas
 
     @staticmethod
     def for_scene(scene_id: int, **kw) -> "RenderParams":
@@ -186,7 +195,7 @@ class RenderParams:
         """QuinEngine viewer frame (GraphicsRTX.cpp:163-193, rtx.hlsl:373-404): 1 spp,
         depth 5 with Russian roulette, vertical FOV 45, no ILLUM / Fresnel Kd,
         gamma-2.2 running mean; `seed` is the 32-bit frame seed."""
-        base = dict(width=800, height=600, spp=1, spp_chunk=1, max_depth=5, illum=1.0, fov_deg=45.0,
+        base = dict(width=640, height=480, spp=1, spp_chunk=1, max_depth=5, illum=1.0, fov_deg=45.0,
                     fresnel_kd=False, seed=0, mode="quinengine")
         base.update(kw)
         return RenderParams(**base)
@@ -213,6 +222,10 @@ class RenderParams:
         p.mode = MODES[self.mode]
         p.lean = 1 if self.lean else 0
         p.wf_sort = 1 if self.wf_sort else 0
+        p.wf_streams, p.wf_refill, p.wf_group_shift = int(self.wf_streams), int(self.wf_refill), int(self.wf_group_shift)
+        p.ready_thresh, p.tail_units_per_lane = int(self.ready_thresh), int(self.tail_units_per_lane)
+        p.tail_units, p.wf_mem_limit = int(self.tail_units), int(self.wf_mem_limit)
+        p.force_peer_copy = 1 if self.force_peer_copy else 0
         return p
 
     def output_pixels(self) -> int:
@@ -232,20 +245,23 @@ class RenderParams:
 class Scene:
     """A device-resident scene (CreateGeometry result + KD tree)."""
 
-    def __init__(self, model: ObjModel, host_only: bool = False, kd_cache: Optional[str] = None):
-        """kd_cache: directory for the on-disk KD-build cache (mcpt_scene_create_cached);
-        ``cache_hit`` tells whether the tree was read from it."""
+    LAYOUTS = {"auto": _capi.LAYOUT_AUTO, "global": _capi.LAYOUT_GLOBAL}
+
+    def __init__(self, model: ObjModel, host_only: bool = False, kd_cache: Optional[str] = None,
+                 layout: str = "auto"):
+        """kd_cache: directory for the on-disk KD-build cache (mcpt_scene_create_ex);
+        ``cache_hit`` tells whether the tree was read from it.  layout "global":
+        the scene image with child-box pair records in global memory even if it
+        would fit in LDS (MCPT_LAYOUT_GLOBAL)."""
+        if layout not in self.LAYOUTS:
+            raise ValueError(f"layout must be one of {sorted(self.LAYOUTS)}")
         h = C.c_void_p()
-        self.cache_hit = False
         if kd_cache:
             os.makedirs(kd_cache, exist_ok=True)
-            hit = C.c_int32(0)
-            check(lib().mcpt_scene_create_cached(model.handle, os.fsencode(kd_cache), int(host_only),
-                                                 C.byref(h), C.byref(hit)))
-            self.cache_hit = bool(hit.value)
-        else:
-            fn = lib().mcpt_scene_create_host if host_only else lib().mcpt_scene_create
-            check(fn(model.handle, C.byref(h)))
+        opt = _capi.SceneOptions(os.fsencode(kd_cache) if kd_cache else None, int(host_only), self.LAYOUTS[layout])
+        hit = C.c_int32(0)
+        check(lib().mcpt_scene_create_ex(model.handle, C.byref(opt), C.byref(h), C.byref(hit)))
+        self.cache_hit = bool(hit.value)
         self._h = h
         self.host_only = host_only
 
@@ -326,6 +342,13 @@ class Scene:
 
     def reserve(self, params: RenderParams):
         check(lib().mcpt_scene_reserve(self.handle, C.byref(params.to_c())))
+
+    def plan(self, params: RenderParams) -> dict:
+        """The scheduling a render of `params` would use (streams, batch, thresholds) and
+        its device memory (mcpt_plan_query); nothing is allocated or launched."""
+        out = _capi.PlanInfo()
+        check(lib().mcpt_plan_query(self.handle, C.byref(params.to_c()), C.byref(out)))
+        return out.as_dict()
 
     def stats(self) -> dict:
         st = RenderStats()

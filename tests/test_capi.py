@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol(mcpt):
 
 def test_abi_version_and_defaults(mcpt):
     from montecarlopathtracer_amd._capi import RenderParamsC, lib
-    assert lib().mcpt_abi_version() == 5
+    assert lib().mcpt_abi_version() == 6
     p = RenderParamsC()
     lib().mcpt_render_params_default(C.byref(p))
     # CV/stdafx.h:41-46, CUTracer.cu:189,212,349-351
@@ -42,6 +42,11 @@ def test_abi_version_and_defaults(mcpt):
     # QE/RTX/GraphicsRTX.cpp:173-193, QE/Shader/rtx.hlsl:400
     assert (q.mode, q.spp, q.max_depth, q.fresnel_kd) == (1, 1, 5, 0)
     assert q.fov_deg == 45.0 and list(q.eye) == [0, 5, 17] and q.illum == 1.0
+    assert (q.width, q.height) == (640, 480)                 # the QE window, QE/Main.cpp:11
+    # scheduling fields default to 0 = automatic
+    for f in ("wf_streams", "wf_refill", "wf_group_shift", "ready_thresh", "tail_units_per_lane", "tail_units",
+              "wf_mem_limit", "force_peer_copy"):
+        assert getattr(p, f) == 0 and getattr(q, f) == 0, f
     # the Python mirror agrees with the C defaults
     r = mcpt.RenderParams.for_quinengine().to_c()
     for f in ("mode", "spp", "max_depth", "fresnel_kd", "fov_deg", "illum", "width", "height"):
@@ -95,7 +100,8 @@ def test_struct_layouts_match_header(mcpt, tmp_path):
     inc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
     structs = {"mcpt_render_params": _capi.RenderParamsC, "mcpt_render_stats": _capi.RenderStats,
                "mcpt_scene_info": _capi.SceneInfo, "mcpt_model_info": _capi.ModelInfo,
-               "mcpt_model_desc": _capi.ModelDesc}
+               "mcpt_model_desc": _capi.ModelDesc, "mcpt_plan_info": _capi.PlanInfo,
+               "mcpt_scene_options": _capi.SceneOptions}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "mcpt.h"', 'int main(void) {']
     for cname, py in structs.items():
         lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')

@@ -104,3 +104,128 @@ def test_pw_tracer_dropin_with_device_list(mcpt, tmp_path):
     host = np.zeros((30, 40, 3), np.float32)
     tr.render_scene(1, host, num_kernels=3, samples_per_kernel=4)
     assert np.array_equal(got, host)
+
+
+@pytest.mark.parametrize("case", range(len(CASES)))
+def test_forced_peer_copy_path(mcpt, devices, case):
+    """render_multi's cross-device branch (hipMemcpyPeerAsync into devices[0]'s
+    gather buffer, capi.cpp) forced between two replicas on one device
+    (mcpt_render_params::force_peer_copy): the single-device image bit for bit,
+    with a progressive second call and through render_device after reserve."""
+    import torch
+    kw = dict(CASES[case])
+    qe = kw.pop("mode", None) == "qe"
+    model = mcpt.ObjModel(mcpt.scene_path("scene01"))
+    mk = (lambda **a: mcpt.RenderParams.for_quinengine(**a)) if qe else (lambda **a: mcpt.RenderParams(**a))
+    devices([0])
+    single = mcpt.Scene(model)
+    ref0, _ = single.render(mk(**kw))
+    ref1, _ = single.render(mk(spp_offset=kw["spp"], prev_count=1, **kw), ref0.copy())
+    devices([0, 0])
+    multi = mcpt.Scene(model)
+    img0, st = multi.render(mk(force_peer_copy=True, **kw))
+    assert st["devices"] == 2
+    assert np.array_equal(img0.view(np.uint32), ref0.view(np.uint32))
+    img1, _ = multi.render(mk(spp_offset=kw["spp"], prev_count=1, force_peer_copy=True, **kw), img0.copy())
+    assert np.array_equal(img1.view(np.uint32), ref1.view(np.uint32))
+    p = mk(force_peer_copy=True, **kw)
+    multi.reserve(p)
+    fb = torch.zeros((p.width * p.height, 4), dtype=torch.float32, device="cuda")
+    multi.render_device(p, fb.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    multi.stats()
+    assert np.array_equal(fb.view(p.height, p.width, 4)[..., :3].cpu().numpy(), ref0)
+
+
+def test_init_without_devices_restores_single_device_scenes(mcpt):
+    """mcpt_init(NULL, 0) after a device list: later scenes are single-device
+    on the current device again (include/mcpt.h)."""
+    from montecarlopathtracer_amd._capi import check, lib
+    tr = mcpt.Tracer()
+    tr.initialize([0, 0])
+    model = mcpt.ObjModel(mcpt.scene_path("scene01"))
+    assert mcpt.Scene(model).info()["n_devices"] == 2
+    check(lib().mcpt_init(None, 0))
+    s = mcpt.Scene(model)
+    assert s.info()["n_devices"] == 1 and s.info()["device"] == 0
+    tr.initialize([0])
+
+
+def test_plan_query_reports_the_schedule(mcpt, devices):
+    """mcpt_plan_query: the automatic scheduling of a render (the bench line's
+    config echoes it) and explicit overrides, without allocating anything."""
+    devices([0])
+    scene = mcpt.Scene(mcpt.ObjModel(mcpt.scene_path("scene01")))
+    c2 = dict(width=1024, height=1024, spp=1024, spp_chunk=32)
+    wf = scene.plan(mcpt.RenderParams(pipeline="wavefront", **c2))
+    assert (wf["pipeline"], wf["variant"], wf["wf_streams"], wf["wf_batch"]) == (1, 4, 3, 1 << 27)
+    assert wf["wf_refill"] == 16 and wf["wf_group_shift"] == 6 and wf["work_paths"] == 1 << 30
+    assert 3 * 160 * (1 << 27) <= wf["workspace_bytes"] < wf["device_free_bytes"]
+    mk = scene.plan(mcpt.RenderParams(**c2))
+    assert mk["pipeline"] == 0 and mk["ready_thresh"] == 32 and mk["tail_units"] > 0 and mk["variant"] in (1, 2)
+    o = scene.plan(mcpt.RenderParams(pipeline="wavefront", wf_streams=2, wf_refill=8, wf_batch=1 << 26, **c2))
+    assert (o["wf_streams"], o["wf_refill"], o["wf_batch"]) == (2, 8, 1 << 26)
+    devices([0, 0])
+    multi = mcpt.Scene(mcpt.ObjModel(mcpt.scene_path("scene01")))
+    m = multi.plan(mcpt.RenderParams(pipeline="wavefront", **c2))
+    assert m["devices"] == 2 and m["peer_access"] == 1 and m["work_paths"] == (1 << 30) // 2
+
+
+def test_wavefront_memory_budget(mcpt):
+    """wf_mem_limit: a default batch shrinks until its queues fit (same image),
+    an explicit batch that does not fit fails with MCPT_E_NOMEM and a message,
+    before anything is launched."""
+    scene = mcpt.Scene(mcpt.ObjModel(mcpt.scene_path("scene01")))
+    kw = dict(width=96, height=64, spp=64, spp_chunk=8, pipeline="wavefront")
+    ref, rs = scene.render(mcpt.RenderParams(**kw))
+    big = scene.plan(mcpt.RenderParams(**kw))
+    lim = big["wf_queue_bytes"] // 2
+    small = scene.plan(mcpt.RenderParams(wf_mem_limit=lim, **kw))
+    assert small["wf_batch"] < big["wf_batch"]
+    img, st = scene.render(mcpt.RenderParams(wf_mem_limit=lim, **kw))
+    assert np.array_equal(img, ref) and st["rays"] == rs["rays"]
+    with pytest.raises(mcpt.McptError) as e:
+        scene.render(mcpt.RenderParams(wf_mem_limit=1 << 20, wf_batch=1 << 20, **kw))
+    assert e.value.code == -5 and "wavefront queues" in str(e.value)
+
+
+def test_global_layout_option_matches_oracle(mcpt, oracle_mod):
+    """MCPT_LAYOUT_GLOBAL (the child-box pair records in global memory) on
+    scene01, which would fit in LDS: both pipelines render the oracle's
+    node-box walk bit for bit with equal counters."""
+    path = mcpt.scene_path("scene01")
+    scene = mcpt.Scene(mcpt.ObjModel(path), layout="global")
+    assert scene.info()["node_boxes"] == 1 and scene.info()["lds_bytes"] == 0
+    W, H, spp, chunk = 48, 40, 6, 3
+    ref, rc = oracle_mod.Scene(path).render(oracle_mod.RenderParams(
+        width=W, height=H, spp=spp, spp_chunk=chunk, threads=8, node_boxes=1))
+    for pipe in ("megakernel", "wavefront"):
+        img, st = scene.render(mcpt.RenderParams(width=W, height=H, spp=spp, spp_chunk=chunk, pipeline=pipe))
+        assert np.array_equal(img, ref), pipe
+        assert st["variant"] == (3 if pipe == "megakernel" else 5)
+        for k in ("rays", "paths", "inner_visits", "leaf_visits", "tri_tests", "shades"):
+            assert st[k] == rc[k], (pipe, k, st[k], rc[k])
+
+
+def test_wavefront_render_captured_in_a_graph(mcpt):
+    """mcpt_scene_reserve creates the wavefront's side streams and events, so
+    a multi-stream wavefront render can be captured into a HIP graph (torch
+    CUDA graph on ROCm) and replayed: the replay writes the direct render's
+    image."""
+    import torch
+    scene = mcpt.Scene(mcpt.ObjModel(mcpt.scene_path("scene01")))
+    p = mcpt.RenderParams(width=128, height=96, spp=16, spp_chunk=8, pipeline="wavefront", wf_streams=2,
+                          wf_batch=128 * 96 * 4)
+    ref, _ = scene.render(p)
+    scene.reserve(p)
+    fb = torch.zeros((128 * 96, 4), dtype=torch.float32, device="cuda")
+    s = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s, capture_error_mode="relaxed"):
+        scene.render_device(p, fb.data_ptr(), s.cuda_stream)
+    for _ in range(2):
+        fb.zero_()
+        g.replay()
+    torch.cuda.synchronize()
+    assert np.array_equal(fb.view(96, 128, 4)[..., :3].cpu().numpy(), ref)

@@ -128,13 +128,13 @@ def test_pw_tracer_adapter_matches_abi(mcpt, tmp_path):
     assert np.array_equal(got, host)
 
 
-@pytest.mark.parametrize("streams", ["1", "2", "3", "4"])
+@pytest.mark.parametrize("streams", [1, 2, 3, 4])
 @pytest.mark.parametrize("batch", [1000, 4096, 20000, 0, 1 << 22])
-def test_wavefront_batches_equal_megakernel(mcpt, monkeypatch, batch, streams):
+def test_wavefront_batches_equal_megakernel(mcpt, batch, streams):
     """Any batch split of the wavefront (partial batches, batches spanning
     several chunks, ragged last chunk, shards, packed shard output) on any
-    number of streams renders the megakernel's image and counts bit for bit."""
-    monkeypatch.setenv("MCPT_WF_STREAMS", streams)
+    number of streams (mcpt_render_params::wf_streams) renders the
+    megakernel's image and counts bit for bit."""
     path = mcpt.scene_path("scene01")
     scene = mcpt.Scene(mcpt.ObjModel(path))
     for kw in ({"width": 61, "height": 45, "spp": 7, "spp_chunk": 3},
@@ -143,7 +143,7 @@ def test_wavefront_batches_equal_megakernel(mcpt, monkeypatch, batch, streams):
                {"width": 72, "height": 40, "spp": 9, "spp_chunk": 2, "shard_count": 4, "shard_index": 3,
                 "packed": True, "tile": 8}):
         mk, smk = scene.render(mcpt.RenderParams(**kw))
-        wf, swf = scene.render(mcpt.RenderParams(pipeline="wavefront", wf_batch=batch, **kw))
+        wf, swf = scene.render(mcpt.RenderParams(pipeline="wavefront", wf_batch=batch, wf_streams=streams, **kw))
         assert np.array_equal(mk, wf)
         for k in ("rays", "paths", "inner_visits", "leaf_visits", "leaf_refs", "tri_tests", "shades"):
             assert smk[k] == swf[k], (k, smk[k], swf[k])
@@ -226,22 +226,19 @@ def test_qe_viewer_adapter_frames(mcpt, tmp_path):
     assert np.array_equal(mcpt.read_png(png), mcpt.encode_8bit(img))
 
 
-@pytest.mark.parametrize("tail", ["0", "1000", "2100", None], ids=["whole-units", "mixed", "mixed-ragged", "default"])
-def test_tail_split_is_bit_identical(mcpt, oracle_mod, monkeypatch, tail):
+@pytest.mark.parametrize("tail", [-1, 1000, 2100, 0], ids=["whole-units", "mixed", "mixed-ragged", "default"])
+def test_tail_split_is_bit_identical(mcpt, oracle_mod, tail):
     """The megakernel's tail split (last units handed out one sample at a time,
     summed in sample order by the reduction) renders the whole-unit image bit
     for bit: no split, a split starting mid-chunk, and the default (every unit
     of a small image).  spp 7 / chunk 3 leaves a ragged last chunk."""
-    if tail is None:
-        monkeypatch.delenv("MCPT_TAIL_UNITS", raising=False)
-    else:
-        monkeypatch.setenv("MCPT_TAIL_UNITS", tail)
+    tk = {"tail_units_per_lane": -1} if tail < 0 else {"tail_units": tail}
     path = mcpt.scene_path("scene01")
     W, H, spp, chunk = 40, 30, 7, 3      # 1200 px x 3 chunks = 3600 units
     ref, rc = _oracle_render(oracle_mod, path, W, H, spp, chunk, 7, 77, 1, 10.0, 1,
                              node_boxes=_node_boxes(mcpt, path))
     scene = mcpt.Scene(mcpt.ObjModel(path))
-    img, st = scene.render(mcpt.RenderParams.for_scene(1, width=W, height=H, spp=spp, spp_chunk=chunk, seed=77))
+    img, st = scene.render(mcpt.RenderParams.for_scene(1, width=W, height=H, spp=spp, spp_chunk=chunk, seed=77, **tk))
     assert np.array_equal(img, ref), f"max abs diff {np.abs(img - ref).max()}"
     for k in ("rays", "paths", "inner_visits", "leaf_visits", "leaf_refs", "tri_tests", "shades"):
         assert st[k] == rc[k], (k, st[k], rc[k])
