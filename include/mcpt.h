@@ -229,6 +229,17 @@ typedef struct {
 } mcpt_model_desc;
 int mcpt_model_create(const mcpt_model_desc* d, mcpt_model** out);
 int mcpt_model_read_obj(const char* path, mcpt_model** out);
+/* The same with a reader flavor: MCPT_OBJ_CVMCTRACER = mcpt_model_read_obj;
+ * MCPT_OBJ_TINYOBJ = what QuinEngine loads through tinyobjloader v1.1.1
+ * (QE/Utils/Structure.hpp:9-12, RTX/ShaderResource.hpp:88-104, 204-215):
+ * materials with tinyobj's defaults (Ka Kd Ks 0, Ns 1, Ni 1; Tr = 1 - dissolve,
+ * `d` wins over `Tr`), shapes in file order, a material per triangle (a group
+ * per run of one shape's faces with one material, keyed "%06d:<shape>"). */
+int mcpt_model_read_obj_ex(const char* path, int32_t flavor, mcpt_model** out);
+enum {
+    MCPT_OBJ_CVMCTRACER = 0,    /* CVMCTracer ObjReader (ObjReader.cpp:8-259) */
+    MCPT_OBJ_TINYOBJ = 1        /* QuinEngine's tinyobjloader */
+};
 void mcpt_model_free(mcpt_model* m);
 int mcpt_model_get_info(const mcpt_model* m, mcpt_model_info* out);
 int mcpt_model_copy_vertices(const mcpt_model* m, float* out);       /* n_vertices*3 */

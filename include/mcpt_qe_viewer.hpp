@@ -3,7 +3,7 @@
 // Stands in for the QuinEngine RTX renderer behind Quin::Core::Graphics
 // (MCRT/QuinEngine/Core/Graphics.hpp:17-20: Initialize / Shutdown / OnUpdate),
 // whose per-frame work is GraphicsRTX::DoOnUpdate (QE/RTX/GraphicsRTX.cpp:163-232):
-//   * scene01 loaded once, KD tree built once                       (:165-167)
+//   * scene01 loaded once (tinyobjloader), KD tree built once        (:165-167)
 //   * camera LookAtRH (0,5,17)->(0,5,16), PerspectiveFovRH(pi/4, W/H) (:173-184)
 //   * frame seed = uniform_int_distribution<unsigned>(mt19937(1234)),
 //     prevCount = frame counter                                        (:168-193)
@@ -32,12 +32,15 @@ public:
     Viewer& operator=(const Viewer&) = delete;
 
     // GraphicsRTX::Initialize + the static scene setup of DoOnUpdate
-    int Initialize(const std::string& obj_path, uint32_t width, uint32_t height, int32_t device = 0) {
+    // QuinEngine reads its scene through tinyobjloader (QE/Utils/Structure.hpp:9-12),
+    // hence the default flavor; its window is 640x480 (QE/Main.cpp:11)
+    int Initialize(const std::string& obj_path, uint32_t width = 640, uint32_t height = 480, int32_t device = 0,
+                   int32_t flavor = MCPT_OBJ_TINYOBJ) {
         Shutdown();
         int rc = mcpt_init(&device, 1);
         if (rc != MCPT_OK) return rc;
         mcpt_model* m = nullptr;
-        rc = mcpt_model_read_obj(obj_path.c_str(), &m);
+        rc = mcpt_model_read_obj_ex(obj_path.c_str(), flavor, &m);
         if (rc != MCPT_OK) return rc;
         rc = mcpt_scene_create(m, &scene_);
         mcpt_model_free(m);

@@ -87,6 +87,8 @@ class SceneOptions(C.Structure):
     _fields_ = [("kd_cache_dir", C.c_char_p), ("host_only", C.c_int32), ("layout", C.c_int32)]
 
 
+OBJ_CVMCTRACER = 0
+OBJ_TINYOBJ = 1
 LAYOUT_AUTO = 0
 LAYOUT_GLOBAL = 1
 
@@ -113,6 +115,7 @@ _SIGS = {
     "mcpt_render_params_quinengine": (None, [C.POINTER(RenderParamsC)]),
     "mcpt_model_create": (C.c_int, [C.POINTER(ModelDesc), C.POINTER(_vp)]),
     "mcpt_model_read_obj": (C.c_int, [C.c_char_p, C.POINTER(_vp)]),
+    "mcpt_model_read_obj_ex": (C.c_int, [C.c_char_p, C.c_int32, C.POINTER(_vp)]),
     "mcpt_model_free": (None, [_vp]),
     "mcpt_model_get_info": (C.c_int, [_vp, C.POINTER(ModelInfo)]),
     "mcpt_model_copy_vertices": (C.c_int, [_vp, C.POINTER(C.c_float)]),

@@ -989,6 +989,17 @@ int mcpt_model_read_obj(const char* path, mcpt_model** out) {
     });
 }
 
+int mcpt_model_read_obj_ex(const char* path, int32_t flavor, mcpt_model** out) {
+    return guarded([&]() -> int {
+        if (!path || !out) return fail(MCPT_E_INVALID, "path/out is NULL");
+        if (flavor != MCPT_OBJ_CVMCTRACER && flavor != MCPT_OBJ_TINYOBJ) return fail(MCPT_E_INVALID, "unknown flavor");
+        auto m = std::make_unique<mcpt_model>();
+        mcpt::read_obj(path, m->m, flavor);
+        *out = m.release();
+        return MCPT_OK;
+    });
+}
+
 void mcpt_model_free(mcpt_model* m) { delete m; }
 
 int mcpt_model_get_info(const mcpt_model* m, mcpt_model_info* out) {

@@ -10,6 +10,7 @@
 #include "host_model.hpp"
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cctype>
 #include <cfloat>
@@ -160,9 +161,169 @@ void read_mtl(ObjModel& m, const std::string& path) {   // ObjReader.cpp:163-259
     });
 }
 
+// tinyobjloader v1.1.1's MTL semantics (QE/3rdparty/include/tiny_obj_loader.h
+// LoadMtl, the loader QuinEngine uses, QE/Utils/Structure.hpp:9-12): every
+// newmtl appends (a lookup finds the first of a name), InitMaterial defaults
+// (Ka Kd Ks 0, shininess 1, ior 1, dissolve 1), Ks does not touch Ns, `d`
+// sets dissolve and wins over `Tr`, which sets dissolve = 1 - Tr; QuinEngine
+// then uploads Tr = 1 - dissolve (RTX/ShaderResource.hpp:204-215), in float.
+void read_mtl_tinyobj(ObjModel& m, const std::string& path) {
+    const std::string text = slurp(path);
+    int idx = -1;
+    bool has_d = false, has_tr = false;
+    float dissolve = 1.0f;
+    std::string tok;
+    auto flush = [&]() {
+        if (idx >= 0) m.materials[static_cast<size_t>(idx)].Tr = static_cast<double>(1.0f - dissolve);
+    };
+    for_each_line(text, [&](const std::string& line) {
+        Cursor c{line.data(), line.data() + line.size()};
+        if (!c.token(tok) || tok[0] == '#') return;
+        if (tok == "newmtl") {
+            flush();
+            c.token(tok);
+            ObjMaterial mt;
+            mt.name = tok;
+            mt.Ns = 1.0;
+            mt.Ni = 1.0;
+            m.materials.push_back(mt);
+            idx = static_cast<int>(m.materials.size()) - 1;
+            has_d = has_tr = false;
+            dissolve = 1.0f;
+            return;
+        }
+        if (idx < 0) return;
+        ObjMaterial& mt = m.materials[static_cast<size_t>(idx)];
+        if (tok == "Ka" || tok == "Kd" || tok == "Ks") {
+            Vec3 v;
+            v.x = static_cast<float>(c.number<double>());
+            v.y = static_cast<float>(c.number<double>());
+            v.z = static_cast<float>(c.number<double>());
+            (tok[1] == 'a' ? mt.Ka : (tok[1] == 'd' ? mt.Kd : mt.Ks)) = v;
+        } else if (tok == "Ns") {
+            mt.Ns = static_cast<float>(c.number<double>());
+        } else if (tok == "Ni") {
+            mt.Ni = static_cast<float>(c.number<double>());
+        } else if (tok == "d") {
+            dissolve = static_cast<float>(c.number<double>());
+            has_d = true;
+        } else if (tok == "Tr") {
+            if (!has_d) dissolve = 1.0f - static_cast<float>(c.number<double>());
+            has_tr = true;
+        }
+    });
+    flush();
+    (void)has_tr;
+}
+
+int find_material_tinyobj(const ObjModel& m, const std::string& name) {   // material_map: the first of a name
+    for (size_t i = 1; i < m.materials.size(); ++i)
+        if (m.materials[i].name == name) return static_cast<int>(i);
+    return 0;                                                                // -1 in tinyobj: the zero material
+}
+
+// tinyobjloader's OBJ semantics (LoadObj, tiny_obj_loader.h:1712-2000), as
+// QuinEngine consumes them (RTX/ShaderResource.hpp:88-104: shapes in file
+// order, a material id per triangle): every `g` / `o` line starts a shape
+// (named by the first name after `g`, the rest of the line after `o`; the
+// first shape is unnamed), `usemtl` switches the per-face material without
+// ending the shape, faces are fan-triangulated (v0, v[k-1], v[k]).  In the
+// ObjModel a group is a run of one shape's faces with one material, keyed
+// "%06d:<shape name>" so the std::map order -- CreateGeometry's order and the
+// brute-force rank -- is the file order, and each geometry's material is its
+// faces' own.  The dummy material 0 (tinyobj's id -1) is all zero, as an
+// out-of-range StructuredBuffer read returns.
+void read_obj_tinyobj(const std::string& path, ObjModel& m) {
+    m = ObjModel();
+    m.path = path;
+    m.vertices.push_back(Vec3{});
+    m.n_texcoords = 1;
+    m.normals.push_back(Vec3{});
+    m.triangles.push_back(ObjTriangle{});
+    ObjMaterial zero;
+    zero.Ns = 0.0;
+    zero.Ni = 0.0;
+    m.materials.push_back(zero);
+    const std::string text = slurp(path);
+    std::string shape_name;
+    int material = 0, run_material = -1, runs = 0;
+    std::vector<int32_t>* group = nullptr;
+    bool new_shape = true;
+    std::string tok;
+    auto face_group = [&]() -> std::vector<int32_t>* {
+        if (new_shape || material != run_material) {
+            char key[32];
+            std::snprintf(key, sizeof key, "%06d:", runs++);
+            group = &m.groups[key + shape_name];
+            run_material = material;
+            new_shape = false;
+        }
+        return group;
+    };
+    for_each_line(text, [&](const std::string& line) {
+        Cursor c{line.data(), line.data() + line.size()};
+        if (!c.token(tok) || tok[0] == '#') return;
+        if (tok == "v" || tok == "vn") {
+            Vec3 v;
+            v.x = static_cast<float>(c.number<double>());
+            v.y = static_cast<float>(c.number<double>());
+            v.z = static_cast<float>(c.number<double>());
+            (tok.size() == 1 ? m.vertices : m.normals).push_back(v);
+        } else if (tok == "vt") {
+            ++m.n_texcoords;
+        } else if (tok == "f") {
+            std::vector<int32_t>* g = face_group();
+            std::vector<std::array<int32_t, 3>> fv;
+            std::string vt;
+            while (c.token(vt)) {
+                int32_t vi, ti, ni;
+                if (!parse_face_vertex(vt, vi, ti, ni)) throw Error{MCPT_E_PARSE, "Invalid OBJ file!"};
+                // negative indices count back from the end (tinyobj fixIndex)
+                if (vi < 0) vi += static_cast<int32_t>(m.vertices.size());
+                if (ti < 0) ti += static_cast<int32_t>(m.n_texcoords);
+                if (ni < 0) ni += static_cast<int32_t>(m.normals.size());
+                fv.push_back({vi, ti, ni});
+            }
+            for (size_t k = 2; k < fv.size(); ++k) {
+                ObjTriangle t;
+                t.material = material;
+                const std::array<int32_t, 3>* q[3] = {&fv[0], &fv[k - 1], &fv[k]};
+                for (int j = 0; j < 3; ++j) { t.v[j] = (*q[j])[0]; t.t[j] = (*q[j])[1]; t.n[j] = (*q[j])[2]; }
+                m.triangles.push_back(t);
+                g->push_back(static_cast<int32_t>(m.triangles.size() - 1));
+            }
+        } else if (tok == "g") {
+            shape_name = c.token(tok) ? tok : std::string();
+            new_shape = true;
+        } else if (tok == "o") {
+            c.skip();
+            shape_name.assign(c.p, c.end);
+            while (!shape_name.empty() && std::isspace(static_cast<unsigned char>(shape_name.back())))
+                shape_name.pop_back();
+            new_shape = true;
+        } else if (tok == "usemtl") {
+            c.token(tok);
+            material = find_material_tinyobj(m, tok);
+        } else if (tok == "mtllib") {
+            c.token(tok);
+            size_t slash = path.find_last_of('/');
+            std::string dir = (slash == std::string::npos) ? std::string(".") : path.substr(0, slash);
+            read_mtl_tinyobj(m, dir + "/" + tok);
+        }
+    });
+}
+
 }  // namespace
 
-void read_obj(const std::string& path, ObjModel& m) {   // ObjReader.cpp:8-161
+void read_obj(const std::string& path, ObjModel& m, int flavor) {
+    if (flavor == MCPT_OBJ_TINYOBJ) {
+        read_obj_tinyobj(path, m);
+        return;
+    }
+    read_obj_cv(path, m);
+}
+
+void read_obj_cv(const std::string& path, ObjModel& m) {   // ObjReader.cpp:8-161
     m = ObjModel();
     m.path = path;
     m.vertices.push_back(Vec3{});

@@ -41,8 +41,11 @@ struct ObjModel {
     std::map<std::string, std::vector<int32_t>> groups;
 };
 
-// Throws mcpt::Error on failure.
-void read_obj(const std::string& path, ObjModel& out);
+// Throws mcpt::Error on failure.  flavor MCPT_OBJ_CVMCTRACER (0): the
+// CVMCTracer ObjReader (read_obj_cv); MCPT_OBJ_TINYOBJ (1): tinyobjloader as
+// QuinEngine uses it (host_model.cpp read_obj_tinyobj).
+void read_obj(const std::string& path, ObjModel& out, int flavor = 0);
+void read_obj_cv(const std::string& path, ObjModel& out);
 
 struct Geometry {                     // Geometry.h:14-35
     Vec3 Ka, Kd, Ks;

@@ -53,25 +53,28 @@ def write_png(path: str, image: np.ndarray) -> None:
 
 
 def read_png(path: str) -> np.ndarray:
-    """Read an 8-bit RGB, non-interlaced PNG (as write_png and OpenCV write them)."""
+    """Read an 8-bit RGB or RGBA, non-interlaced PNG (as write_png, OpenCV and
+    D3DX11SaveTextureToFile write them): (H, W, 3) or (H, W, 4) uint8."""
     data = open(path, "rb").read()
     if data[:8] != b"\x89PNG\r\n\x1a\n":
         raise ValueError("not a PNG file")
     pos, idat = 8, b""
     w = h = 0
+    nc = 3
     while pos < len(data):
         n, tag = struct.unpack(">I4s", data[pos:pos + 8])
         body = data[pos + 8:pos + 8 + n]
         if tag == b"IHDR":
             w, h, depth, ctype, _, _, interlace = struct.unpack(">IIBBBBB", body)
-            if depth != 8 or ctype != 2 or interlace:
-                raise ValueError("only 8-bit RGB non-interlaced PNGs are supported")
+            if depth != 8 or ctype not in (2, 6) or interlace:
+                raise ValueError("only 8-bit RGB / RGBA non-interlaced PNGs are supported")
+            nc = 3 if ctype == 2 else 4
         elif tag == b"IDAT":
             idat += body
         pos += 12 + n
-    raw = np.frombuffer(zlib.decompress(idat), np.uint8).reshape(h, 1 + 3 * w)
-    out = np.zeros((h, 3 * w), np.int32)
-    prev = np.zeros(3 * w, np.int32)
+    raw = np.frombuffer(zlib.decompress(idat), np.uint8).reshape(h, 1 + nc * w)
+    out = np.zeros((h, nc * w), np.int32)
+    prev = np.zeros(nc * w, np.int32)
     for y in range(h):
         ft, line = raw[y, 0], raw[y, 1:].astype(np.int32)
         if ft in (0, 2):                     # none / up: whole row at once
@@ -79,18 +82,17 @@ def read_png(path: str) -> np.ndarray:
             out[y] = cur
             prev = cur
             continue
-        cur = np.zeros(3 * w, np.int32)
-        for x in range(3 * w):
-            a = cur[x - 3] if x >= 3 else 0
+        cur = np.zeros(nc * w, np.int32)
+        if ft == 1:                          # sub: a running sum per channel
+            cur = (np.cumsum(line.reshape(w, nc), axis=0) & 0xFF).reshape(-1)
+            out[y] = cur
+            prev = cur
+            continue
+        for x in range(nc * w):
+            a = cur[x - nc] if x >= nc else 0
             b = prev[x]
-            c = prev[x - 3] if x >= 3 else 0
-            if ft == 0:
-                p = 0
-            elif ft == 1:
-                p = a
-            elif ft == 2:
-                p = b
-            elif ft == 3:
+            c = prev[x - nc] if x >= nc else 0
+            if ft == 3:
                 p = (a + b) // 2
             else:
                 pa, pb, pc = abs(b - c), abs(a - c), abs(a + b - 2 * c)
@@ -98,7 +100,7 @@ def read_png(path: str) -> np.ndarray:
             cur[x] = (line[x] + p) & 0xFF
         out[y] = cur
         prev = cur
-    return out.reshape(h, w, 3).astype(np.uint8)
+    return out.reshape(h, w, nc).astype(np.uint8)
 
 
 def write_pfm(path: str, hostcolor: np.ndarray) -> None:

@@ -44,15 +44,21 @@ def _fptr(a):
 class ObjModel:
     """PW::FileReader::ObjModel (ObjReader.hpp:37-63): OBJ/MTL data with dummy index 0."""
 
-    def __init__(self, path: Optional[str] = None):
+    FLAVORS = {"cvmctracer": _capi.OBJ_CVMCTRACER, "tinyobj": _capi.OBJ_TINYOBJ}
+
+    def __init__(self, path: Optional[str] = None, flavor: str = "cvmctracer"):
+        """flavor "tinyobj": read as QuinEngine does through tinyobjloader
+        (mcpt_model_read_obj_ex, include/mcpt.h) -- use it for qe_scene01."""
         self._h = None
         self.path = None
         if path is not None:
-            self.read_obj(path)
+            self.read_obj(path, flavor)
 
-    def read_obj(self, path: str) -> bool:   # ObjModel::readObj (ObjReader.cpp:8)
+    def read_obj(self, path: str, flavor: str = "cvmctracer") -> bool:   # ObjModel::readObj (ObjReader.cpp:8)
+        if flavor not in self.FLAVORS:
+            raise ValueError(f"flavor must be one of {sorted(self.FLAVORS)}")
         h = C.c_void_p()
-        check(lib().mcpt_model_read_obj(path.encode(), C.byref(h)))
+        check(lib().mcpt_model_read_obj_ex(path.encode(), self.FLAVORS[flavor], C.byref(h)))
         self._free()
         self._h = h
         self.path = path

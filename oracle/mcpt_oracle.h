@@ -85,6 +85,8 @@ typedef struct {
 
 /* scene ------------------------------------------------------------------ */
 orc_scene* orc_scene_load(const char* obj_path, char* err, int errlen);
+/* flavor 0: the CVMCTracer ObjReader; 1: QuinEngine's tinyobjloader (obj_reader.c) */
+orc_scene* orc_scene_load_ex(const char* obj_path, int flavor, char* err, int errlen);
 void orc_scene_free(orc_scene* s);
 /* info[0..9] = nverts, nnormals, ntris(incl. dummy), nmats, ngroups,
  *              ngeoms, nkd_tris, nnodes, nleaf_ids, kd_depth              */

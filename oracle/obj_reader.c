@@ -12,6 +12,10 @@
  *  - face vertex forms v, v/t, v//n, v/t/n (ObjReader.hpp:90-138);
  *  - MTL: newmtl reuses an existing name (ObjReader.cpp:196-205); Ka/Kd/Ks
  *    floats, Ks also sets Ns=2 (:225-233); Ns/Tr/Ni doubles (:235-254).
+ * orc_model_read_tinyobj restates, independently of the product reader, how
+ * QuinEngine loads a scene through tinyobjloader v1.1.1 (tiny_obj_loader.h
+ * LoadObj / LoadMtl; QE/Utils/Structure.hpp:9-12, RTX/ShaderResource.hpp:
+ * 88-104, 204-215) -- see that function.
  */
 #include "oracle_internal.h"
 
@@ -302,6 +306,160 @@ int orc_model_read(orc_model* m, const char* path, char* err, int errlen) {
     free(text);
     if (!ok) return 0;
     qsort(m->groups, (size_t)m->ngroups, sizeof(orc_group), group_cmp);   /* std::map order */
+    return 1;
+}
+
+/* ---- tinyobjloader flavor -------------------------------------------------
+ * MTL (LoadMtl): every newmtl appends, a lookup finds the first of a name;
+ * defaults Ka Kd Ks 0, shininess 1, ior 1, dissolve 1; `d` sets dissolve and
+ * wins over `Tr` (dissolve = 1 - Tr); Ks leaves Ns alone; QuinEngine uploads
+ * Tr = 1 - dissolve (float).  OBJ (LoadObj): `g` / `o` start a shape, `usemtl`
+ * changes the per-face material id within it, fan triangulation (v0, v[k-1],
+ * v[k]), negative indices from the end.  Shapes keep file order: each run of
+ * one shape's faces with one material becomes a group "%06d:<shape>" (map
+ * order = file order), so CreateGeometry sees QuinEngine's triangle order
+ * and each triangle's own material.  Material 0 (id -1) is all zero. */
+static int read_mtl_tinyobj(orc_model* m, const char* path, char* err, int errlen) {
+    char* text = slurp(path);
+    if (!text) { snprintf(err, errlen, "Can't open file %s", path); return 0; }
+    line_reader lr = {text, NULL, 0};
+    int idx = -1, has_d = 0;
+    float dissolve = 1.0f;
+    char tok[512];
+    while (next_line(&lr)) {
+        istr s = {lr.line, 0};
+        if (!get_token(&s, tok, sizeof tok)) continue;
+        if (tok[0] == '#') continue;
+        if (!strcmp(tok, "newmtl")) {
+            if (idx >= 0) m->mats[idx].Tr = (double)(1.0f - dissolve);
+            get_token(&s, tok, sizeof tok);
+            orc_mat mt;
+            mat_init(&mt, tok);
+            mt.Ns = 1.0; mt.Tr = 0.0; mt.Ni = 1.0;
+            PUSH(m->mats, m->nmats, m->cap_mats, mt);
+            idx = m->nmats - 1;
+            has_d = 0;
+            dissolve = 1.0f;
+            continue;
+        }
+        if (idx < 0) continue;
+        orc_mat* mt = &m->mats[idx];
+        if (!strcmp(tok, "Ka") || !strcmp(tok, "Kd") || !strcmp(tok, "Ks")) {
+            orc_v3 v;
+            v.x = (float)get_number(&s, 0); v.y = (float)get_number(&s, 0); v.z = (float)get_number(&s, 0);
+            if (tok[1] == 'a') mt->Ka = v;
+            else if (tok[1] == 'd') mt->Kd = v;
+            else mt->Ks = v;
+        } else if (!strcmp(tok, "Ns")) {
+            mt->Ns = (float)get_number(&s, 0);
+        } else if (!strcmp(tok, "Ni")) {
+            mt->Ni = (float)get_number(&s, 0);
+        } else if (!strcmp(tok, "d")) {
+            dissolve = (float)get_number(&s, 0);
+            has_d = 1;
+        } else if (!strcmp(tok, "Tr")) {
+            if (!has_d) dissolve = 1.0f - (float)get_number(&s, 0);
+        }
+    }
+    if (idx >= 0) m->mats[idx].Tr = (double)(1.0f - dissolve);
+    free(lr.line);
+    free(text);
+    return 1;
+}
+
+int orc_model_read_tinyobj(orc_model* m, const char* path, char* err, int errlen) {
+    memset(m, 0, sizeof *m);
+    orc_v3 zero = {0, 0, 0};
+    PUSH(m->verts, m->nverts, m->cap_verts, zero);
+    PUSH(m->normals, m->nnormals, m->cap_normals, zero);
+    m->ntexcoords = 1;
+    orc_tri t0;
+    memset(&t0, 0, sizeof t0);
+    PUSH(m->tris, m->ntris, m->cap_tris, t0);
+    orc_mat m0;
+    memset(&m0, 0, sizeof m0);                 /* all zero, Ns and Ni too */
+    PUSH(m->mats, m->nmats, m->cap_mats, m0);
+
+    char* text = slurp(path);
+    if (!text) { snprintf(err, errlen, "Can't open file %s", path); return 0; }
+    char shape[512] = "";
+    int mat = 0, run_mat = -1, runs = 0, grp = -1, fresh = 1;
+    line_reader lr = {text, NULL, 0};
+    char tok[512];
+    int ok = 1;
+    int* fv = NULL;
+    int nfv = 0, cap_fv = 0;
+    while (ok && next_line(&lr)) {
+        istr s = {lr.line, 0};
+        if (!get_token(&s, tok, sizeof tok)) continue;
+        if (tok[0] == '#') continue;
+        if (!strcmp(tok, "mtllib")) {
+            get_token(&s, tok, sizeof tok);
+            const char* slash = strrchr(path, '/');
+            char mpath[4096];
+            if (slash) snprintf(mpath, sizeof mpath, "%.*s/%s", (int)(slash - path), path, tok);
+            else snprintf(mpath, sizeof mpath, "./%s", tok);
+            if (!read_mtl_tinyobj(m, mpath, err, errlen)) ok = 0;
+        } else if (!strcmp(tok, "g")) {
+            if (!get_token(&s, shape, sizeof shape)) shape[0] = 0;
+            fresh = 1;
+        } else if (!strcmp(tok, "o")) {
+            skip_ws(&s);
+            snprintf(shape, sizeof shape, "%s", s.p);
+            size_t n = strlen(shape);
+            while (n && isspace((unsigned char)shape[n - 1])) shape[--n] = 0;
+            fresh = 1;
+        } else if (!strcmp(tok, "usemtl")) {
+            get_token(&s, tok, sizeof tok);
+            mat = find_material(m, tok);
+        } else if (!strcmp(tok, "f")) {
+            if (fresh || mat != run_mat) {
+                char key[600];
+                snprintf(key, sizeof key, "%06d:%s", runs++, shape);
+                grp = find_add_group(m, key);
+                run_mat = mat;
+                fresh = 0;
+            }
+            nfv = 0;
+            while (get_token(&s, tok, sizeof tok)) {
+                int vi, ti, ni;
+                if (!parse_face_vertex(tok, &vi, &ti, &ni)) {
+                    snprintf(err, errlen, "Invalid OBJ file!");
+                    ok = 0;
+                    break;
+                }
+                if (vi < 0) vi += m->nverts;
+                if (ti < 0) ti += m->ntexcoords;
+                if (ni < 0) ni += m->nnormals;
+                PUSH(fv, nfv, cap_fv, vi);
+                PUSH(fv, nfv, cap_fv, ti);
+                PUSH(fv, nfv, cap_fv, ni);
+            }
+            for (int k = 2; ok && k < nfv / 3; k++) {
+                orc_tri t;
+                const int q[3] = {0, k - 1, k};
+                for (int j = 0; j < 3; j++) {
+                    t.v[j] = fv[3 * q[j]]; t.t[j] = fv[3 * q[j] + 1]; t.n[j] = fv[3 * q[j] + 2];
+                }
+                t.mat = mat;
+                PUSH(m->tris, m->ntris, m->cap_tris, t);
+                orc_group* g = &m->groups[grp];
+                PUSH(g->tris, g->ntris, g->cap, m->ntris - 1);
+            }
+        } else if (!strcmp(tok, "v") || !strcmp(tok, "vn")) {
+            float x = (float)get_number(&s, 0), y = (float)get_number(&s, 0), z = (float)get_number(&s, 0);
+            orc_v3 v = {x, y, z};
+            if (tok[1] == 0) PUSH(m->verts, m->nverts, m->cap_verts, v);
+            else PUSH(m->normals, m->nnormals, m->cap_normals, v);
+        } else if (!strcmp(tok, "vt")) {
+            m->ntexcoords++;
+        }
+    }
+    free(fv);
+    free(lr.line);
+    free(text);
+    if (!ok) return 0;
+    qsort(m->groups, (size_t)m->ngroups, sizeof(orc_group), group_cmp);   /* "%06d:" keys: file order */
     return 1;
 }
 

@@ -58,6 +58,8 @@ def lib():
         vp, f32p, i32p, u32p = C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_int32), C.POINTER(C.c_uint32)
         L.orc_scene_load.restype = vp
         L.orc_scene_load.argtypes = [C.c_char_p, C.c_char_p, C.c_int]
+        L.orc_scene_load_ex.restype = vp
+        L.orc_scene_load_ex.argtypes = [C.c_char_p, C.c_int, C.c_char_p, C.c_int]
         L.orc_scene_free.argtypes = [vp]
         L.orc_scene_info.argtypes = [vp, C.POINTER(C.c_int64)]
         for n in ("orc_copy_vertices", "orc_copy_normals"):
@@ -117,10 +119,11 @@ def _p(a, ct):
 class Scene:
     """An oracle scene (model + CreateGeometry groups + reference KD tree)."""
 
-    def __init__(self, obj_path: str):
+    def __init__(self, obj_path: str, flavor: str = "cvmctracer"):
+        """flavor "tinyobj": QuinEngine's loader semantics (obj_reader.c orc_model_read_tinyobj)"""
         L = lib()
         err = C.create_string_buffer(512)
-        h = L.orc_scene_load(obj_path.encode(), err, 512)
+        h = L.orc_scene_load_ex(obj_path.encode(), {"cvmctracer": 0, "tinyobj": 1}[flavor], err, 512)
         if not h:
             raise RuntimeError(f"oracle: {err.value.decode()}")
         self._h = h

@@ -927,12 +927,17 @@ int orc_render(const orc_scene* s, const orc_params* p, float* out, orc_counters
 }
 
 /* ============================ scene assembly ============================== */
-orc_scene* orc_scene_load(const char* path, char* err, int errlen) {
+orc_scene* orc_scene_load(const char* path, char* err, int errlen) { return orc_scene_load_ex(path, 0, err, errlen); }
+
+orc_scene* orc_scene_load_ex(const char* path, int flavor, char* err, int errlen) {
     char dummy[256];
     if (!err) { err = dummy; errlen = sizeof dummy; }
     err[0] = 0;
     orc_scene* s = calloc(1, sizeof(orc_scene));
-    if (!orc_model_read(&s->model, path, err, errlen)) { orc_scene_free(s); return NULL; }
+    if (!(flavor == 1 ? orc_model_read_tinyobj : orc_model_read)(&s->model, path, err, errlen)) {
+        orc_scene_free(s);
+        return NULL;
+    }
     orc_model* m = &s->model;
     /* CreateGeometry (CUTracer.cu:277-311): non-empty groups in map order */
     s->geoms = calloc((size_t)(m->ngroups ? m->ngroups : 1), sizeof(orc_geom));

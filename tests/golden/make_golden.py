@@ -12,6 +12,18 @@ it reads /root/reference, which does not exist on the GPU box).
   oracle_scene01_32x24.npz
                         a small oracle render (regression fixture for the
                         oracle itself; not a reference output).
+  mcdocx_fig3_scene2_blinn_phong.png, mcdocx_fig4_scene2_phong.png
+                        MC.docx Figures 3 and 4 (word/media/image7.png and
+                        image9.png of the .docx zip), byte copies.
+  qe_result.png         the reference's own QuinEngine render
+                        (MCRT/QuinEngine/result.png, 640x480), byte copy.
+  qe_scene01_tinyobj.npz
+                        what tinyobjloader reads from QuinEngine's own scene
+                        (MCRT/QuinEngine/Res/scene01.obj + its scene01.mtl).
+  result1step_blocks.npz
+                        50x50-pixel block means (8-bit units) of the reference's
+                        progressive ladder result1step/step00000{0..9}.png and
+                        the blocks saturated (>= 254) in any step (tests/ladder.py).
 """
 import os
 import shutil
@@ -72,7 +84,7 @@ def main():
     from montecarlopathtracer_amd.scenes import scene_path
     subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle", "ref")], check=True)
     tool = os.path.join(ROOT, "oracle", "_ref", "tinyobj_dump")
-    for sc in ("scene01", "scene02", "scene03"):
+    for sc in ("scene01", "scene02", "scene03", "qe_scene01"):
         p = scene_path(sc)
         out = f"/tmp/{sc}_tobj.bin"
         subprocess.run([tool, p, os.path.dirname(p) + "/", out], check=True)
@@ -89,6 +101,25 @@ def main():
     shutil.copy(f"{REF}/CVMCTracer/CVMCTracer/result1.png", os.path.join(HERE, "result1.png"))
     shutil.copy(f"{REF}/CVMCTracer/CVMCTracer/result1step/step000000.png",
                 os.path.join(HERE, "result1_step000000.png"))
+    # MC.docx figures (a zip member each) and the QuinEngine render, byte copies
+    import zipfile
+    with zipfile.ZipFile(f"{REF}/MC.docx") as z:
+        for member, name in (("word/media/image7.png", "mcdocx_fig3_scene2_blinn_phong.png"),
+                             ("word/media/image9.png", "mcdocx_fig4_scene2_phong.png")):
+            with open(os.path.join(HERE, name), "wb") as f:
+                f.write(z.read(member))
+    shutil.copy(f"{REF}/MCRT/QuinEngine/result.png", os.path.join(HERE, "qe_result.png"))
+    # the progressive ladder as block means
+    from PIL import Image
+    sys.path.insert(0, os.path.dirname(HERE))
+    from ladder import block_means
+    steps = [np.asarray(Image.open(f"{REF}/CVMCTracer/CVMCTracer/result1step/step{k:06d}.png").convert("RGB"))
+             for k in range(10)]
+    sat = np.zeros(block_means(steps[0]).shape[:2], bool)
+    for a in steps:
+        sat |= block_means((a >= 254).astype(np.float64)).max(axis=2) > 0
+    np.savez_compressed(os.path.join(HERE, "result1step_blocks.npz"),
+                        means=np.stack([block_means(a) for a in steps]), saturated=sat)
     import oracle
     s = oracle.Scene(scene_path("scene01"))
     p = oracle.RenderParams(width=32, height=24, spp=4, spp_chunk=2, traversal=oracle.BRUTE, threads=4)

@@ -319,3 +319,43 @@ def test_runaway_kd_build_and_non_finite_vertices_are_refused(mcpt, tmp_path):
     with pytest.raises(mcpt.McptError) as e:
         mcpt.Scene(mcpt.ObjModel(str(bad)), host_only=True)
     assert e.value.code == -1 and "non-finite" in str(e.value)
+
+
+@pytest.mark.parametrize("name", SCENES + ["qe_scene01"])
+def test_tinyobj_flavor_matches_reference_tinyobjloader(mcpt, oracle_mod, name):
+    """mcpt_model_read_obj_ex(MCPT_OBJ_TINYOBJ) -- QuinEngine's loader semantics
+    (QE/Utils/Structure.hpp:9-12, RTX/ShaderResource.hpp:88-104, 204-215) --
+    against what the reference's own tinyobjloader v1.1.1 reads
+    (tests/golden/<scene>_tinyobj.npz): vertices, face indices, the per-face
+    material ids, shapes in file order with their face counts, and every
+    material value (Ka Kd Ks Ns Ni exact, Tr = 1 - dissolve in float); the
+    oracle's independent restatement reads the same model, geometries and KD
+    tree.  qe_scene01 is QuinEngine's own scene (its MTL: emitter Ka 0.80 and
+    no Kd; spheres without Kd / Ka)."""
+    g = np.load(os.path.join(GOLDEN, f"{name}_tinyobj.npz"))
+    m = mcpt.ObjModel(mcpt.scene_path(name), flavor="tinyobj")
+    v, n, t, mt = m.vertices(), m.normals(), m.triangles(), m.materials()
+    assert np.allclose(v[1:], g["vertices"], rtol=2e-7, atol=1e-12)
+    assert np.allclose(n[1:], g["normals"], rtol=2e-7, atol=1e-12)
+    idx = g["indices"].reshape(-1, 3, 3)
+    assert np.array_equal(t[1:, 0:3] - 1, idx[:, :, 0]) and np.array_equal(t[1:, 6:9] - 1, idx[:, :, 2])
+    assert np.array_equal(t[1:, 9] - 1, g["material_ids"])                   # tinyobj id -1 -> dummy 0
+    shapes = []
+    for key, tris in m.groups().items():                                     # runs in file order
+        shape = key.split(":", 1)[1]
+        if shapes and shapes[-1][0] == shape and shapes[-1][2] == tris[0] - 1:
+            shapes[-1] = (shape, shapes[-1][1] + len(tris), tris[-1])
+        else:
+            shapes.append((shape, len(tris), tris[-1]))
+    assert [(s, c) for s, c, _ in shapes] == list(zip(g["shape_names"].tolist(), g["shape_faces"].tolist()))
+    mv = g["mat_values"]                                                     # Ka Kd Ks shininess dissolve ior
+    assert mt.shape[0] - 1 == mv.shape[0] and not mt[0].any()
+    assert np.array_equal(mt[1:, 0:9].astype(np.float32), mv[:, 0:9])
+    assert np.array_equal(mt[1:, 9].astype(np.float32), mv[:, 9])
+    assert np.array_equal(mt[1:, 10].astype(np.float32), (np.float32(1) - mv[:, 10]).astype(np.float32))
+    assert np.array_equal(mt[1:, 11].astype(np.float32), mv[:, 11])
+    o = oracle_mod.Scene(mcpt.scene_path(name), flavor="tinyobj")
+    for f in ("vertices", "normals", "triangles", "materials"):
+        assert np.array_equal(getattr(o, f)(), getattr(m, f)()), f
+    nodes, _, kdt, geoms = mcpt.Scene(m, host_only=True).kd()
+    assert np.array_equal(nodes, o.kd_nodes()) and np.array_equal(kdt, o.kd_tris()) and np.array_equal(geoms, o.geoms())
