@@ -54,9 +54,10 @@ def algorithmic_bytes(st: dict, pixels: int) -> dict:
     return {"survey": survey, "own": own}
 
 
-def _workload_args(args) -> list:
+def _workload_args(args, shard=(1, 0)) -> list:
     return ["--scene", args.scene, "--width", str(args.width), "--height", str(args.height), "--spp", str(args.spp),
-            "--spp-chunk", str(args.spp_chunk), "--pipeline", args.pipeline, "--wf-batch", str(args.wf_batch)] + \
+            "--spp-chunk", str(args.spp_chunk), "--pipeline", args.pipeline, "--wf-batch", str(args.wf_batch),
+            "--wf-streams", str(args.wf_streams), "--pmc-shard", f"{shard[0]},{shard[1]}"] + \
         (["--counting"] if args.counting else [])
 
 
@@ -84,7 +85,7 @@ def read_wf_kernels(d: str) -> dict:
     return {c: {"ns": sum(v["ns"].values()), "dispatches": len(v["ns"]), **v["counters"]} for c, v in out.items()}
 
 
-def pmc_pass(args, counters: list, tag: str, timeout_s: int = 150, reader=None) -> dict:
+def pmc_pass(args, counters: list, tag: str, timeout_s: int = 150, reader=None, shard=(1, 0)) -> dict:
     """One rocprofv3 PMC pass over ONE render of the same workload, in a child
     process (MI355X_MICROARCH.md 'rocprofv3 PMC slots': one pass per counter
     group -- FETCH_SIZE uses 3 of the 4 TCC slots, WRITE_SIZE 2).  Returns the
@@ -99,7 +100,7 @@ def pmc_pass(args, counters: list, tag: str, timeout_s: int = 150, reader=None) 
     from pmc_summary import read_counters
     out = tempfile.mkdtemp(prefix=f"mcpt_pmc_{tag}_", dir="/tmp")
     cmd = ["rocprofv3", "--pmc", *counters, "--output-format", "csv", "-d", out, "-o", "run", "--",
-           sys.executable, os.path.abspath(__file__), "--pmc-child"] + _workload_args(args)
+           sys.executable, os.path.abspath(__file__), "--pmc-child"] + _workload_args(args, shard)
     env = dict(os.environ, TMPDIR="/tmp")
     for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
@@ -113,6 +114,12 @@ def pmc_pass(args, counters: list, tag: str, timeout_s: int = 150, reader=None) 
         return {}
     try:
         vals = (reader or read_counters)(out) if proc.returncode == 0 else {}
+        if args.keep_pmc and proc.returncode == 0:   # the raw csv behind the line, for profiles/
+            import glob
+            dst = os.path.join(args.keep_pmc, tag)
+            os.makedirs(dst, exist_ok=True)
+            for f in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
+                shutil.copy(f, os.path.join(dst, os.path.basename(f)))
     finally:
         shutil.rmtree(out, ignore_errors=True)
     return vals
@@ -130,14 +137,14 @@ def live_counters(args) -> dict:
     return c
 
 
-def wavefront_hbm(args) -> dict:
+def wavefront_hbm(args, shard=(1, 0)) -> dict:
     """Measured HBM bytes and time of each wavefront kernel over one render
     (FETCH_SIZE doubled + WRITE_SIZE, as live_counters): the queue streams are
     where this pipeline meets the HBM roofline."""
-    f = pmc_pass(args, ["FETCH_SIZE"], "wf_fetch", reader=read_wf_kernels)
-    w = pmc_pass(args, ["WRITE_SIZE"], "wf_write", reader=read_wf_kernels)
+    f = pmc_pass(args, ["FETCH_SIZE"], "wf_fetch", reader=read_wf_kernels, shard=shard)
+    w = pmc_pass(args, ["WRITE_SIZE"], "wf_write", reader=read_wf_kernels, shard=shard)
     v = pmc_pass(args, ["SQ_INSTS_VALU", "SQ_THREAD_CYCLES_VALU", "SQ_ACTIVE_INST_VALU", "SQ_WAVE_CYCLES",
-                        "GRBM_GUI_ACTIVE"], "wf_valu", reader=read_wf_kernels)
+                        "GRBM_GUI_ACTIVE"], "wf_valu", reader=read_wf_kernels, shard=shard)
     res = {}
     for cls in f:
         if cls not in w or "FETCH_SIZE" not in f[cls] or "WRITE_SIZE" not in w[cls]:
@@ -287,6 +294,14 @@ def main():
     ap.add_argument("--pipeline", choices=["megakernel", "wavefront"], default="wavefront")
     ap.add_argument("--no-alt", action="store_true", help="skip the other pipeline's comparison timing (N = 1)")
     ap.add_argument("--wf-batch", type=int, default=0)
+    ap.add_argument("--wf-streams", type=int, default=0, help="wavefront streams (0 = the library's default)")
+    ap.add_argument("--single-process", action="store_true",
+                    help="one process drives all --gpus devices through mcpt_init(devices) (the C ABI's "
+                         "multi-device render: replicas, peer-copy gather) instead of one rank per GPU")
+    ap.add_argument("--devices", default="", help="--single-process device list (default 0..gpus-1); a repeated "
+                                                  "ordinal rehearses the multi-device path on one GPU, e.g. 0,0")
+    ap.add_argument("--keep-pmc", default="", help="copy the raw rocprofv3 PMC csv files into this directory")
+    ap.add_argument("--pmc-shard", default="1,0", help=argparse.SUPPRESS)   # PMC child: shard count,index
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = this process's CPU share (<= 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -306,6 +321,8 @@ def main():
     # GPUs this box has (local % device_count) and the gather staged through host
     # memory; the driver's multi-GPU runs use the default, RCCL ("nccl").
     backend = os.environ.get("MCPT_DIST_BACKEND", "nccl")
+    if world > 1 and args.single_process:
+        raise SystemExit("--single-process drives every GPU from one process: launch it without torch.distributed.run")
     if world > 1:
         local = local % max(torch.cuda.device_count(), 1) if backend == "gloo" else local
         torch.cuda.set_device(local)
@@ -316,29 +333,42 @@ def main():
     dev = torch.device("cuda", local if world > 1 else 0)
     red_dev = dev if backend == "nccl" else torch.device("cpu")   # device of the small timing reductions
     torch.cuda.set_device(dev)
-    M.Tracer().initialize([dev.index])
+    # --single-process: one process, the C ABI's device list (mcpt_init): scenes are
+    # replicated on every device and each render is split into interleaved-tile
+    # shards gathered to device 0 by peer copies (capi.cpp render_multi)
+    n_dev = args.gpus if args.single_process else 1
+    devices = [int(x) for x in args.devices.split(",")] if args.devices else list(range(n_dev))
+    if args.single_process and (len(devices) != n_dev or max(devices) >= torch.cuda.device_count()):
+        raise SystemExit(f"--single-process --gpus {n_dev}: device list {devices}, "
+                         f"{torch.cuda.device_count()} device(s) visible")
+    M.Tracer().initialize(devices if n_dev > 1 else [dev.index])
+    n_gpus = world * n_dev
 
     scene = M.Scene(M.ObjModel(M.scene_path(args.scene)))
     scene_id = 2 if args.scene in ("scene02", "scene03") else 1
-    if args.pmc_child:   # PMC pass: exactly one render of the timed kernel, then exit
+    if args.pmc_child:   # PMC pass: exactly one render of the timed kernel (rank 0's shard), then exit
+        sc, si = (int(x) for x in args.pmc_shard.split(","))
         p = M.RenderParams.for_scene(scene_id, width=args.width, height=args.height, spp=args.spp,
                                      spp_chunk=args.spp_chunk, tile=8, pipeline=args.pipeline, wf_batch=args.wf_batch,
+                                     wf_streams=args.wf_streams, shard_count=sc, shard_index=si, packed=sc > 1,
                                      lean=not args.counting)
         fb = torch.zeros((p.output_pixels(), 4), dtype=torch.float32, device=dev)
         scene.render_device(p, fb.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
         torch.cuda.synchronize(dev)
         return
-    # timed renders run the megakernel lean (no per-step traversal counters, same
+    # timed renders run the lean kernels (no per-step traversal counters, same
     # image and ray count); the node/leaf/triangle counts of the bytes model come
     # from one untimed counting render of the same frame (they are deterministic)
     lean = not args.counting
     p = M.RenderParams.for_scene(scene_id, width=args.width, height=args.height, spp=args.spp,
                                  spp_chunk=args.spp_chunk, tile=8, shard_count=world, shard_index=rank,
-                                 packed=world > 1, pipeline=args.pipeline, wf_batch=args.wf_batch, lean=lean)
+                                 packed=world > 1, pipeline=args.pipeline, wf_batch=args.wf_batch,
+                                 wf_streams=args.wf_streams, lean=lean)
     p_count = dataclasses.replace(p, lean=False)
     n_out = p.output_pixels()
     fb = torch.zeros((n_out, 4), dtype=torch.float32, device=dev)
     scene.reserve(p)
+    plan = scene.plan(p)
     stream = torch.cuda.current_stream(dev)
 
     gatherer = None
@@ -370,7 +400,8 @@ def main():
     for _ in range(args.steps):
         step()
     ev1.record(stream)
-    torch.cuda.synchronize(dev)
+    for d in sorted(set(devices)) if n_dev > 1 else [dev]:
+        torch.cuda.synchronize(d)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -378,7 +409,7 @@ def main():
 
     # the other pipeline on the same frame, for comparison (N = 1; same image, bit for bit)
     alt = None
-    if world == 1 and not args.no_alt:
+    if n_gpus == 1 and not args.no_alt:
         other = "megakernel" if args.pipeline == "wavefront" else "wavefront"
         pa = dataclasses.replace(p, pipeline=other)
         for _ in range(max(args.warmup, 1)):
@@ -422,59 +453,73 @@ def main():
         mray = rays / elapsed / 1e6
         workload = f"cornell_{args.width}x{args.height}_{args.spp}spp" + ("" if args.scene == "scene01" else
                                                                             f"_{args.scene}")
+        cus = torch.cuda.get_device_properties(dev).multi_processor_count
+        # the PMC passes profile one device's share: rank 0's shard (N > 1) or the whole frame
+        shard = (n_gpus, 0) if n_gpus > 1 else (1, 0)
         roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
-                "traffic": None, "traffic_unit": "GB of HBM read+write per path-kernel launch",
-                "source": "rocprofv3 --pmc passes of this build and workload, run by this bench"}
-        if world == 1 and not args.no_pmc and args.pipeline == "wavefront":
-            # per-kernel measured HBM traffic; `achieved` = the whole pipeline's bytes / the frame's
-            # kernel time (HIP events of the timed renders: the streams overlap kernels, while the
-            # PMC passes serialize them, so each kernel's own ms/GBps there is its time alone)
-            kh = wavefront_hbm(args)
-            if kh:
-                tot_b = sum((k["hbm_read_GB"] + k["hbm_write_GB"]) for k in kh.values())
-                gbs = tot_b / (kern_ms * 1e-3) if kern_ms > 0 else 0.0
-                roof.update(achieved=round(gbs, 2), frac=round(gbs / HBM_PEAK_GBS, 5), traffic=round(tot_b, 3),
-                            traffic_unit="GB of HBM read+write per frame (all wavefront kernels)", kernels=kh,
-                            kernels_note="per-kernel ms / GBps from the PMC passes, which run kernels one at a "
-                                         "time; the timed frame overlaps them on several streams; frac_of_copy "
-                                         "can exceed 1 for read-mostly kernels (accumulate): the copy reference "
-                                         "moves equal read and write bytes")
-                ext = kh.get("extend", {})
-                vb = valu_block(ext.pop("valu_counters", {}), torch.cuda.get_device_properties(dev).multi_processor_count,
-                                ext.get("ms", 0.0), per_launch["rays"])
-                for k in kh.values():
-                    k.pop("valu_counters", None)
+                "traffic": None, "traffic_unit": None,
+                "source": "rocprofv3 --pmc passes of this build and workload, run by this bench"
+                          + (f" on rank 0's shard ({shard[1]} of {shard[0]})" if n_gpus > 1 else "")}
+        if not args.no_pmc and args.pipeline == "wavefront":
+            # the dominant kernel is wf_extend (the traversal): `achieved` = its measured HBM bytes
+            # (FETCH_SIZE x2 + WRITE_SIZE of its dispatches over one frame) / the same dispatches'
+            # duration in the PMC pass, which serializes the kernels; the whole pipeline's queue
+            # traffic over the frame's HIP-event time is reported separately under `pipeline`
+            kh = wavefront_hbm(args, shard)
+            ext = kh.get("extend")
+            if ext:
+                eb = ext["hbm_read_GB"] + ext["hbm_write_GB"]
+                gbs = eb / (ext["ms"] * 1e-3) if ext["ms"] > 0 else 0.0
+                roof.update(achieved=round(gbs, 2), frac=round(gbs / HBM_PEAK_GBS, 5), traffic=round(eb, 3),
+                            traffic_unit="GB of HBM read+write per frame by wf_extend's dispatches",
+                            kernel="wf_extend (the traversal, the dominant kernel)",
+                            launches=ext["launches"], kernel_ms=ext["ms"],
+                            avg_launch_ms=round(ext["ms"] / max(ext["launches"], 1), 4),
+                            timing="sum of the extend dispatches' durations in the PMC pass (kernels serialized)")
+                vb = valu_block(ext.pop("valu_counters", {}), cus, ext.get("ms", 0.0), per_launch["rays"] / n_gpus)
                 if vb:
                     vb["kernel"] = "wf_extend (the traversal: the dominant kernel), run alone"
                     roof["valu"] = vb
-        elif world == 1 and not args.no_pmc:
+            for k in kh.values():
+                k.pop("valu_counters", None)
+            if kh:
+                tot_b = sum((k["hbm_read_GB"] + k["hbm_write_GB"]) for k in kh.values())
+                pg = tot_b / (kern_ms * 1e-3) if kern_ms > 0 else 0.0
+                roof["pipeline"] = {
+                    "achieved": round(pg, 2), "frac": round(pg / HBM_PEAK_GBS, 5), "unit": "GB/s",
+                    "traffic": round(tot_b, 3), "traffic_unit": "GB of HBM per frame, all wavefront kernels "
+                                                                "(mostly the SoA queue streams)",
+                    "frame_ms": round(kern_ms, 3), "kernels": kh,
+                    "note": "per-kernel ms / GBps from the PMC passes, which run kernels one at a time; the timed "
+                            "frame overlaps them on several streams (frame_ms = HIP events of the timed renders)"}
+        elif not args.no_pmc:
             # measured HBM bytes: FETCH_SIZE x2 (gfx950 streaming-read undercount) + WRITE_SIZE, KiB
             pmc = live_counters(args)
             if "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
                 hbm = (2.0 * pmc["FETCH_SIZE"] + pmc["WRITE_SIZE"]) * 1024.0
                 gbs = hbm / (kern_ms * 1e-3) / 1e9
                 roof.update(achieved=round(gbs, 2), frac=round(gbs / HBM_PEAK_GBS, 5), traffic=round(hbm / 1e9, 3),
+                            traffic_unit="GB of HBM read+write per path-kernel launch", kernel="path_kernel",
                             hbm_read_GB=round(2.0 * pmc["FETCH_SIZE"] * 1024 / 1e9, 3),
                             hbm_write_GB=round(pmc["WRITE_SIZE"] * 1024 / 1e9, 3))
-            vb = valu_block(pmc, torch.cuda.get_device_properties(dev).multi_processor_count, kern_ms,
-                            per_launch["rays"])
+            vb = valu_block(pmc, cus, kern_ms, per_launch["rays"] / n_gpus)
             if vb:
                 roof["valu"] = vb
-        if world == 1:
-            cb = copy_bandwidth(dev)
-            if roof["achieved"] is not None and cb["GBps"] > 0:
-                cb["achieved_frac"] = round(roof["achieved"] / cb["GBps"], 5)
-            roof["peak_copy_measured"] = cb
-            for k in roof.get("kernels", {}).values():
-                k["frac_of_copy"] = round(k["GBps"] / cb["GBps"], 4) if cb["GBps"] > 0 else None
+        cb = copy_bandwidth(dev)
+        if roof["achieved"] is not None and cb["GBps"] > 0:
+            cb["achieved_frac"] = round(roof["achieved"] / cb["GBps"], 5)
+        roof["peak_copy_measured"] = cb
+        for k in roof.get("pipeline", {}).get("kernels", {}).values():
+            k["frac_of_copy"] = round(k["GBps"] / cb["GBps"], 4) if cb["GBps"] > 0 else None
         in_lds = st["variant"] in (1, 2, 4)   # kernel variants that hold the scene image in LDS
         if not in_lds:
             roof["binding_resource"] = ("memory latency of the node / triangle reads (scene image in global memory, "
                                         "served by L1/L2/MALL; profiles/r02/c4_mem)")
         elif args.pipeline == "wavefront":
-            roof["binding_resource"] = ("extend (the traversal): VALU issue and lane divergence, scene image in LDS; "
-                                        "HBM carries the SoA queue streams, which generate / shade / accumulate "
-                                        "move at 55-100% of the measured copy rate beside the extend")
+            roof["binding_resource"] = ("wf_extend: VALU issue x lane use (valu.useful_lane_frac; scene image in "
+                                        "LDS, so its HBM bytes are ray reads and hit writes only); the queue "
+                                        "streams that generate / shade / accumulate move beside it are under "
+                                        "pipeline")
         else:
             roof["binding_resource"] = ("VALU issue and lane divergence (the scene image is LDS-resident; HBM "
                                         "carries only stack spills and the framebuffer partials)")
@@ -486,16 +531,24 @@ def main():
                                "own_layout_GBps": round(ab["own"] / (kern_ms * 1e-3) / 1e9, 1),
                                "per_ray": {k: round(per_launch[k] / max(per_launch["rays"], 1), 3) for k in
                                            ("inner_visits", "leaf_visits", "leaf_refs", "tri_tests", "shades")}}
+        sched = {k: plan[k] for k in ("wf_streams", "wf_batch", "wf_refill", "wf_group_shift") if
+                 args.pipeline == "wavefront"} if args.pipeline == "wavefront" else \
+            {k: plan[k] for k in ("ready_thresh", "tail_units")}
+        sched["workspace_GB"] = round(plan["workspace_bytes"] / 1e9, 2)
+        if n_gpus > 1:
+            par = (f"pixel-tiles x{n_gpus} + " + (f"{'rccl' if backend == 'nccl' else backend} gather" if world > 1
+                                                  else f"peer-copy gather (one process, mcpt_init({devices}))"))
+        else:
+            par = "pixel-tiles x1"
         line = {
-            "metric": METRIC, "value": round(mray, 3), "unit": "Mray/s", "n_gpus": world, "steps": args.steps,
+            "metric": METRIC, "value": round(mray, 3), "unit": "Mray/s", "n_gpus": n_gpus, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f32",
             "data": f"bundled reference scene {args.scene}.obj (Cornell Box), synthetic camera/seed",
             "config": {"workload": workload, "scene": args.scene,
                        "width": args.width, "height": args.height, "spp": args.spp, "max_depth": 7,
-                       "spp_chunk": args.spp_chunk, "parallelism": f"pixel-tiles x{world}" +
-                       (f" + {'rccl' if backend == 'nccl' else backend} gather" if world > 1 else ""), "pipeline": args.pipeline,
-                       "kernel_variant": st["variant"]},
+                       "spp_chunk": args.spp_chunk, "parallelism": par, "pipeline": args.pipeline,
+                       "kernel_variant": st["variant"], "schedule": sched},
             "rays_per_step": rays // args.steps,
             "paths_per_step": st["paths"] // args.steps,
             "mpath_s": round(st["paths"] / elapsed / 1e6, 3),
@@ -511,7 +564,7 @@ def main():
             "cpu_baseline": None,
             "other_pipeline": alt,
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if n_gpus == 1 and not args.no_cpu_baseline:
             # the GPU's own C1 frame, for the ray-count check of the CPU run
             s1 = scene if args.scene == "scene01" else M.Scene(M.ObjModel(M.scene_path("scene01")))
             _, c1 = s1.render(M.RenderParams(width=512, height=512, spp=16, spp_chunk=32))

@@ -149,7 +149,7 @@ __device__ __forceinline__ uint32_t slot_pid(const WfParams& wf, uint32_t g, uin
 #ifndef MCPT_WF_IMPLICIT0
 #define MCPT_WF_IMPLICIT0 2
 #endif
-__device__ __forceinline__ bool implicit0(const KernelParams& kp, const WfParams& wf) {
+__host__ __device__ __forceinline__ bool implicit0(const KernelParams& kp, const WfParams& wf) {
     return MCPT_WF_IMPLICIT0 && !wf.sort && kp.mode != kModeQE;
 }
 // MCPT_WF_HIT_ID = 1 (default, queue order): extend writes only the hit
@@ -441,6 +441,205 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
     if (tid < 4) cn->cls[tid] = lcnt[tid];
 }
 
+// ---- extend of bounce 0, wave-coherent (CV mode, queue-order shade) ---------
+// Primary rays share the eye as their origin, and generate deals them in
+// 64-path groups -- one 8x8 tile of one sample -- so a wave takes one group
+// and walks the KD tree ONCE for its 64 rays: the node is wave-uniform (read
+// by one LDS broadcast), each lane keeps its own interval, hit and an active
+// flag, and the wave enters a child if any lane's interval reaches it.  With
+// a common origin every lane has the same near side at every split plane (an
+// origin exactly on the plane leaves only lanes inside the plane needing both
+// children, and their near child is the left one), so the wave's front-to-back
+// order is each lane's own: a lane is active at exactly the nodes its own
+// ordered walk (trav_iter) visits, with the same interval and best hit there,
+// and it stops at the same pop.  Hits, visit and test counts are therefore
+// those of the per-ray walk, bit for bit; only the schedule differs (one
+// wave-uniform descent per node instead of 64 divergent ones).
+// Stack: the per-ray walk's lazy LDS stack (S entries in LDS, older ones in
+// the spill area) with a wave-uniform position; a lane's copy of an entry
+// carries its interval, or tmax = NaN if the lane is not in that subtree.
+#ifndef MCPT_WF_PACKET0
+#define MCPT_WF_PACKET0 1
+#endif
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+
+template <int S, int BLOCK, bool COUNT>
+__global__ void __launch_bounds__(BLOCK) wf_extend_primary(const KernelParams kp, const WfParams wf) {
+    static_assert((BLOCK & (BLOCK - 1)) == 0, "stack slot addresses (slot_of) mask by a power-of-two block");
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t g = blockIdx.x;
+    WfCounters* cn = wf.cnt + (size_t)wf.bounce * wf.nseg + g;
+    const uint32_t count = g < wf.nseg ? cn->queued : 0u;
+    if (count == 0) {
+        if (g < wf.nseg && threadIdx.x < 4) cn->cls[threadIdx.x] = 0;
+        return;
+    }
+    const int tid = (int)threadIdx.x;
+    const int lane = tid & 63;
+    const GpuScene& sc = kp.scene;
+    // LDS: [stack S x BLOCK x 16 B | scene image | group counter]
+    unsigned char* const lds_image = smem + (size_t)S * BLOCK * 16;
+    uint32_t* lgrp = reinterpret_cast<uint32_t*>(lds_image + sc.image_bytes);
+    if (tid == 0) *lgrp = 0;
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(sc.image);
+        uint4* dst = reinterpret_cast<uint4*>(lds_image);
+        const uint32_t n16 = sc.image_bytes / 16u;
+        for (uint32_t i = (uint32_t)tid; i < n16; i += BLOCK) dst[i] = src[i];
+    }
+    const float4* tris = reinterpret_cast<const float4*>(lds_image + sc.off_tris);
+    const uint2* nodes = reinterpret_cast<const uint2*>(lds_image + sc.off_nodes) + 1;
+    const uint32_t* leafs = reinterpret_cast<const uint32_t*>(lds_image + sc.off_leafs);
+    __syncthreads();
+    uint4* st = reinterpret_cast<uint4*>(smem) + tid;
+    uint4* spill = kp.spill + (blockIdx.x * BLOCK + (uint32_t)tid);
+    const uint32_t spill_stride = kp.total_lanes;
+    const size_t seg0 = (size_t)g * wf.seg;
+    float4* qb = wf.q[0];
+    const uint32_t qs = wf.slot_stride;
+    const int32_t U = BLOCK * 16;                      // one stack position (see slot_of)
+    const V3 eye = v3(kp.eye[0], kp.eye[1], kp.eye[2]);
+    Counters c = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (;;) {
+        uint32_t grp = 0;
+        if (lane == 0) grp = atomicAdd(lgrp, 1u);
+        const uint32_t base = uni((uint32_t)__shfl((int)grp, 0)) << 6;   // this wave's 64-slot group
+        if (base >= count) break;
+        const uint32_t slot = base + (uint32_t)lane;
+        RayState r;
+        r.o = eye;
+        r.d = v3(0, 0, 1);
+        r.htri = -1;
+        bool active = false, done = false;
+        if (slot < count) {
+            const float4 d4 = ldq(&qb[qf(seg0 + slot, 1, qs)]);
+            if (__float_as_uint(d4.w) != kNoRay) {
+                r.d = xyz(d4);
+                active = begin_ray(r, sc, kp.best_init);
+            }
+        }
+        uint32_t w0 = sc.root_w[0], w1 = sc.root_w[1];  // the wave's node
+        int32_t sp = 0, lo = 0;                         // wave-uniform stack positions
+        if (__ballot(active)) {
+            for (;;) {
+                if ((w0 >> 30) != 3u) {
+                    // ---- inner node: each lane's step of isect_kd_ordered ----
+                    if constexpr (COUNT) c.inner += active ? 1u : 0u;
+                    const uint32_t left = w0 & 0x3FFFFFFFu;
+                    const uint4 pr = *reinterpret_cast<const uint4*>(nodes + left);
+                    const int a = (int)(w0 >> 30);
+                    const float sv = __uint_as_float(w1);
+                    const float oa = sel3(a, eye.x, eye.y, eye.z);
+                    const float ia = sel3(a, r.ix, r.iy, r.iz);
+                    const float t = (sv - oa) * ia;
+                    const bool on_plane = oa == sv;            // wave-uniform (common origin)
+                    bool below = oa < sv, pp = false;
+                    if (on_plane) {
+                        const float da = sel3(a, r.d.x, r.d.y, r.d.z);
+                        below = da <= 0.0f;
+                        pp = da == 0.0f;
+                    }
+                    const float te = t * kEpsHi;
+                    const bool no = !(t > 0.0f) | (t > r.tmax);
+                    const bool fo = te < r.tmin;
+                    const bool go_far = !pp & !no & fo;
+                    const bool push_it = pp | (!pp & !no & !fo);
+                    const bool need_near = active & !go_far, need_far = active & (go_far | push_it);
+                    const float near_max = push_it ? min_qnan(te, r.tmax) : r.tmax;   // near: [tmin, near_max]
+                    const float far_min = go_far ? r.tmin : max_qnan(t, r.tmin);      // far: [far_min, tmax]
+                    // the wave's order: left first iff the (common) near side is the left
+                    const bool first_left = on_plane | (oa < sv);
+                    const bool near_first = below == first_left;
+                    const bool need1 = near_first ? need_near : need_far;
+                    const bool need2 = near_first ? need_far : need_near;
+                    const float lo1 = near_first ? r.tmin : far_min, hi1 = near_first ? near_max : r.tmax;
+                    const float lo2 = near_first ? far_min : r.tmin, hi2 = near_first ? r.tmax : near_max;
+                    const uint32_t f0 = first_left ? pr.x : pr.z, f1 = first_left ? pr.y : pr.w;
+                    const uint32_t s0 = first_left ? pr.z : pr.x, s1 = first_left ? pr.w : pr.y;
+                    if (__ballot(need1)) {
+                        if (__ballot(need2)) {                   // push the second child
+                            lds_uint4* sl = slot_of<S>(st, BLOCK, sp);
+                            if (sp - lo == S * U) {              // LDS part full: its oldest entry to memory
+                                spill[((uint32_t)lo / (uint32_t)U) * spill_stride] = ld4(sl);
+                                lo += U;
+                                if constexpr (COUNT) c.spills++;
+                            }
+                            st4(sl, make_uint4(s0, s1, __float_as_uint(lo2),
+                                               need2 ? __float_as_uint(hi2) : 0x7FC00001u));
+                            sp += U;
+                        }
+                        w0 = f0;
+                        w1 = f1;
+                        active = need1;
+                        r.tmin = lo1;
+                        r.tmax = hi1;
+                    } else {
+                        w0 = s0;
+                        w1 = s1;
+                        active = need2;
+                        r.tmin = lo2;
+                        r.tmax = hi2;
+                    }
+                    continue;
+                }
+                // ---- leaf: the active lanes test its triangles, two per round ----
+                {
+                    const uint32_t lpos = w0 & 0x3FFFFFFFu, lend = lpos + w1;
+                    if constexpr (COUNT) c.leaf += active ? 1u : 0u;
+                    for (uint32_t i = lpos; i < lend; i += 2u) {
+                        const bool two = lend - i >= 2u;
+                        const uint32_t k0 = leafs[i], k1n = leafs[i + 1u];
+                        const uint32_t k1 = two ? k1n : k0;
+                        const float4 a0 = tris[k0], a1 = tris[k0 + 1], a2 = tris[k0 + 2];
+                        const float4 b0 = tris[k1], b1 = tris[k1 + 1], b2 = tris[k1 + 2];
+                        if (active) {
+                            test_tri_pair(r, a0, a1, a2, k0, b0, b1, b2, k1, two);
+                            if constexpr (COUNT) {
+                                c.refs += two ? 2u : 1u;
+                                c.tests += two ? 2u : 1u;
+                            }
+                        }
+                    }
+                }
+                // ---- pop until an entry with an active lane (or the stack is empty) ----
+                bool more = false;
+                while (sp > 0) {
+                    sp -= U;
+                    uint4 e;
+                    if (sp < lo) {                               // LDS part empty: the entry is in memory
+                        e = spill[((uint32_t)sp / (uint32_t)U) * spill_stride];
+                        lo = sp;
+                    } else {
+                        e = ld4(slot_of<S>(st, BLOCK, sp));
+                    }
+                    w0 = uni(e.x);
+                    w1 = uni(e.y);
+                    const float emin = __uint_as_float(e.z), emax = __uint_as_float(e.w);
+                    active = false;
+                    if ((emax == emax) & !done) {                // this lane's own entry (pop_entry)
+                        if (r.best <= emin * kEpsLo) {
+                            done = true;                         // its walk ends here
+                        } else {
+                            active = true;
+                            r.tmin = emin;
+                            r.tmax = emax;
+                        }
+                    }
+                    if (__ballot(active)) {
+                        more = true;
+                        break;
+                    }
+                }
+                if (!more) break;
+            }
+        }
+        if (slot < count) reinterpret_cast<int32_t*>(qb + qf(0, 2, qs))[seg0 + slot] = r.htri;
+    }
+    flush_counters(c, kp.stats);
+    __syncthreads();
+    if (tid < 4) cn->cls[tid] = 0;
+}
+
 // ---- shade: each segment's class lists back to back (CUTracer.cu:105-175) ---
 // Items of segment g are taken in the order [diffuse, phong, fresnel,
 // terminate]; the i-th continuing item writes its next ray to slot i of the
@@ -648,6 +847,16 @@ __global__ void __launch_bounds__(256) wf_accumulate(const KernelParams kp, cons
     kp.partial[(size_t)(wf.chunk_index + j) * kp.npix_local + wf.v0 + u] = make_float4(part.x, part.y, part.z, 0.0f);
 }
 
+template <int S, int BLOCK>
+hipError_t launch_extend_primary(const KernelParams& kp, const WfParams& wf, int grid, size_t lds, hipStream_t st) {
+    auto kern = kp.lean ? wf_extend_primary<S, BLOCK, false> : wf_extend_primary<S, BLOCK, true>;
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(BLOCK), lds, st, kp, wf);
+    return hipGetLastError();
+}
+
 template <bool IN_LDS, int S, int BLOCK>
 hipError_t launch_extend(const KernelParams& kp, const WfParams& wf, int grid, size_t lds, hipStream_t st) {
     auto kern = wf.sort ? (kp.lean ? wf_extend<IN_LDS, S, BLOCK, false, true> : wf_extend<IN_LDS, S, BLOCK, true, true>)
@@ -747,7 +956,13 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams* wf_in, co
             if ((e = hipGetLastError()) != hipSuccess) break;
             for (int b = 0; b < max_bounces && e == hipSuccess; b++) {
                 wf.bounce = b;
-                if (in_lds)
+                // bounce 0 of CV mode (implicit queue 0: every origin is the eye): the
+                // wave-coherent extend, one tree walk per 64-ray tile (MCPT_WF_PACKET0)
+                const bool packet = MCPT_WF_PACKET0 && b == 0 && in_lds && MCPT_WF_IMPLICIT0 >= 2 &&
+                                    implicit0(kb, wf) && wf.group_shift == 6u;
+                if (packet)
+                    e = launch_extend_primary<4, kLdsBlock>(kb, wf, (int)nseg, lds_bytes_in_lds(img, 4) + 32, bs);
+                else if (in_lds)
                     e = launch_extend<true, 4, kLdsBlock>(kb, wf, (int)nseg, lds_bytes_in_lds(img, 4) + 32, bs);
                 else
                     e = launch_extend<false, 8, kGlobalBlock>(kb, wf, (int)nseg, (size_t)8 * kGlobalBlock * 16 + 32,

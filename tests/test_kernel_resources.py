@@ -71,7 +71,8 @@ def test_shipped_kernels_fit_16_waves_per_cu(tmp_path):
     path = {k: v for k, v in kernels.items() if "path_kernel" in k}
     extend = {k: v for k, v in kernels.items() if "wf_extend" in k}
     assert len(path) == 18, sorted(path)  # 3 layouts x (DBG, QE, COUNT) variants
-    assert len(extend) == 8, sorted(extend)   # 2 layouts x (lean, counting) x (queue order, sorted)
+    # 2 layouts x (lean, counting) x (queue order, sorted), + the wave-coherent bounce-0 extend (lean, counting)
+    assert len(extend) == 10, sorted(extend)
     for name, r in {**path, **extend}.items():
         assert r["vgpr"] + r["agpr"] <= 128, (name, r)
         # product variants: the DBG unit-counter megakernels (template arg 4 true) may spill
