@@ -176,7 +176,7 @@ class RenderParams:
     shard_index: int = 0
     packed: bool = False
     pipeline: str = "megakernel"      # or "wavefront" (C5): identical image, different kernels
-    wf_batch: int = 0                 # wavefront paths in flight per batch, 0 = 2^27 (2^28 global scenes)
+    wf_batch: int = 0                 # wavefront paths per batch and stream, 0 = automatic (include/mcpt.h)
     mode: str = "cvmctracer"          # or "quinengine": rtx.hlsl path semantics (see for_quinengine)
     lean: bool = False                # kernels without traversal counters (same image; bench timing)
     wf_sort: bool = False             # wavefront: material-sorted shade (class lists); same image
