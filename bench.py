@@ -58,7 +58,20 @@ def _workload_args(args, shard=(1, 0)) -> list:
     return ["--scene", args.scene, "--width", str(args.width), "--height", str(args.height), "--spp", str(args.spp),
             "--spp-chunk", str(args.spp_chunk), "--pipeline", args.pipeline, "--wf-batch", str(args.wf_batch),
             "--wf-streams", str(args.wf_streams), "--pmc-shard", f"{shard[0]},{shard[1]}"] + \
-        (["--counting"] if args.counting else [])
+        [x for kv in args.set for x in ("--set", kv)] + (["--counting"] if args.counting else [])
+
+
+SCHED_FIELDS = ("wf_refill", "wf_group_shift", "ready_thresh", "tail_units_per_lane", "tail_units", "wf_mem_limit")
+
+
+def _tuning(args) -> dict:
+    out = {}
+    for kv in args.set:
+        k, _, v = kv.partition("=")
+        if k not in SCHED_FIELDS:
+            raise SystemExit(f"--set {kv}: field must be one of {SCHED_FIELDS}")
+        out[k] = int(v)
+    return out
 
 
 WF_KERNELS = (("wf_extend", "extend"), ("wf_shade", "shade"), ("wf_generate", "generate"),
@@ -300,6 +313,9 @@ def main():
                          "multi-device render: replicas, peer-copy gather) instead of one rank per GPU")
     ap.add_argument("--devices", default="", help="--single-process device list (default 0..gpus-1); a repeated "
                                                   "ordinal rehearses the multi-device path on one GPU, e.g. 0,0")
+    ap.add_argument("--set", action="append", default=[], metavar="FIELD=VALUE",
+                    help="set a scheduling field of the render params (wf_refill, ready_thresh, wf_group_shift, "
+                         "tail_units_per_lane, wf_mem_limit, ...; never changes the image) -- for sweeps")
     ap.add_argument("--keep-pmc", default="", help="copy the raw rocprofv3 PMC csv files into this directory")
     ap.add_argument("--pmc-shard", default="1,0", help=argparse.SUPPRESS)   # PMC child: shard count,index
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -351,7 +367,7 @@ def main():
         p = M.RenderParams.for_scene(scene_id, width=args.width, height=args.height, spp=args.spp,
                                      spp_chunk=args.spp_chunk, tile=8, pipeline=args.pipeline, wf_batch=args.wf_batch,
                                      wf_streams=args.wf_streams, shard_count=sc, shard_index=si, packed=sc > 1,
-                                     lean=not args.counting)
+                                     lean=not args.counting, **_tuning(args))
         fb = torch.zeros((p.output_pixels(), 4), dtype=torch.float32, device=dev)
         scene.render_device(p, fb.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
         torch.cuda.synchronize(dev)
@@ -363,7 +379,7 @@ def main():
     p = M.RenderParams.for_scene(scene_id, width=args.width, height=args.height, spp=args.spp,
                                  spp_chunk=args.spp_chunk, tile=8, shard_count=world, shard_index=rank,
                                  packed=world > 1, pipeline=args.pipeline, wf_batch=args.wf_batch,
-                                 wf_streams=args.wf_streams, lean=lean)
+                                 wf_streams=args.wf_streams, lean=lean, **_tuning(args))
     p_count = dataclasses.replace(p, lean=False)
     n_out = p.output_pixels()
     fb = torch.zeros((n_out, 4), dtype=torch.float32, device=dev)
