@@ -40,20 +40,6 @@
 #include "render_launch.hpp"
 #include "trace_device.hpp"
 
-// Experiment (off in the product): between bounces of a global-memory scene,
-// sort each segment's continuing rays by the triangle their origin lies on
-// (triangles are numbered in KD-leaf order, so this is an origin-coherent
-// order) with a device radix sort, to measure what origin coherence buys the
-// memory-latency-bound extend.
-#ifndef MCPT_WF_EXP_SORT
-#define MCPT_WF_EXP_SORT 0
-#endif
-#if MCPT_WF_EXP_SORT
-#include <hipcub/hipcub.hpp>
-namespace mcpt {
-__device__ uint32_t* g_exp_keys = nullptr;
-}
-#endif
 
 namespace mcpt {
 
@@ -767,9 +753,6 @@ __global__ void __launch_bounds__(BLOCK) wf_shade_slots(const KernelParams kp, c
     for (uint32_t base = 0; base < total; base += BLOCK) {      // block-uniform trip count
         const uint32_t i = base + threadIdx.x;
         bool cont = false;
-#if MCPT_WF_EXP_SORT
-        uint32_t hit_of_lane = 0;
-#endif
         uint32_t pid = 0, depth = kNoRay, sd = 0;
         V3 o = v3(0, 0, 0), d = v3(0, 0, 0), color = v3(0, 0, 0);
         if (i < total) {
@@ -826,9 +809,6 @@ __global__ void __launch_bounds__(BLOCK) wf_shade_slots(const KernelParams kp, c
                     term = false;
                 }
                 if (!term) {
-#if MCPT_WF_EXP_SORT
-                    hit_of_lane = (uint32_t)htri;
-#endif
                     c.shades++;
                     o = xyz(o4);
                     d = xyz(d4);
@@ -855,27 +835,6 @@ __global__ void __launch_bounds__(BLOCK) wf_shade_slots(const KernelParams kp, c
                 stq(&qb2[qf(ji, 0, qs)], pack(o, pid));
                 stq(&qb2[qf(ji, 1, qs)], pack(d, depth + 1u));
                 stq(&qb2[qf(ji, 3, qs)], pack(color, sd));
-#if MCPT_WF_EXP_SORT
-                {   // Morton code (6/6/5 bits) of the new origin in the root box
-                    const float* lo = sc.root_min;
-                    const float* hi = sc.root_max;
-                    auto q = [](float v, float a, float b, uint32_t n) {
-                        float u = (v - a) / (b - a);
-                        u = u < 0.0f ? 0.0f : (u > 0.999999f ? 0.999999f : u);
-                        return (uint32_t)(u * (float)n);
-                    };
-                    const uint32_t qx = q(o.x, lo[0], hi[0], 64), qy = q(o.y, lo[1], hi[1], 64),
-                                   qz = q(o.z, lo[2], hi[2], 32);
-                    uint32_t mk = 0;
-                    for (int bit = 5; bit >= 0; --bit) {
-                        mk = (mk << 1) | ((qx >> bit) & 1u);
-                        mk = (mk << 1) | ((qy >> bit) & 1u);
-                        if (bit < 5) mk = (mk << 1) | ((qz >> bit) & 1u);
-                    }
-                    (void)hit_of_lane;
-                    g_exp_keys[ji] = (g << 17) | (mk & 0x1FFFEu);
-                }
-#endif
             }
         }
     }
@@ -896,64 +855,6 @@ __global__ void __launch_bounds__(256) wf_accumulate(const KernelParams kp, cons
     kp.partial[(size_t)(wf.chunk_index + j) * kp.npix_local + wf.v0 + u] = make_float4(part.x, part.y, part.z, 0.0f);
 }
 
-#if MCPT_WF_EXP_SORT
-__global__ void exp_init_keys(uint32_t n, uint32_t seg, uint32_t* keys, uint32_t* vals) {
-    for (uint32_t j = blockIdx.x * 256u + threadIdx.x; j < n; j += gridDim.x * 256u) {
-        keys[j] = ((j / seg) << 17) | 0x1FFFFu;
-        vals[j] = j;
-    }
-}
-__global__ void exp_permute(uint32_t n, uint32_t qs, const uint32_t* vals, const float4* q, float4* tmp) {
-    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
-        const uint32_t j = vals[i];
-        tmp[qf(i, 0, n)] = q[qf(j, 0, qs)];
-        tmp[qf(i, 1, n)] = q[qf(j, 1, qs)];
-        tmp[qf(i, 2, n)] = q[qf(j, 3, qs)];
-    }
-}
-__global__ void exp_copy_back(uint32_t n, uint32_t qs, const float4* tmp, float4* q) {
-    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
-        q[qf(i, 0, qs)] = tmp[qf(i, 0, n)];
-        q[qf(i, 1, qs)] = tmp[qf(i, 1, n)];
-        q[qf(i, 3, qs)] = tmp[qf(i, 2, n)];
-    }
-}
-struct ExpSortBufs {
-    uint32_t *keys = nullptr, *keys2 = nullptr, *vals = nullptr, *vals2 = nullptr;
-    float4* tmp = nullptr;
-    void* cub = nullptr;
-    size_t cub_bytes = 0, n = 0;
-};
-ExpSortBufs g_exp[kMaxWfStreams];
-// before shade(b): keys of every slot of queue b+1 = "no ray" of its segment
-hipError_t exp_sort_pre(int h, uint32_t n, uint32_t seg, hipStream_t st) {
-    ExpSortBufs& B = g_exp[h];
-    if (B.n < n) {
-        hipFree(B.keys); hipFree(B.keys2); hipFree(B.vals); hipFree(B.vals2); hipFree(B.tmp); hipFree(B.cub);
-        hipMalloc(&B.keys, n * 4); hipMalloc(&B.keys2, n * 4); hipMalloc(&B.vals, n * 4); hipMalloc(&B.vals2, n * 4);
-        hipMalloc(&B.tmp, (size_t)n * 48);
-        B.cub_bytes = 0;
-        hipcub::DeviceRadixSort::SortPairs(nullptr, B.cub_bytes, B.keys, B.keys2, B.vals, B.vals2, (int)n, 0, 27, st);
-        hipMalloc(&B.cub, B.cub_bytes);
-        B.n = n;
-    }
-    uint32_t* kp = B.keys;
-    hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(g_exp_keys), &kp, sizeof kp, 0, hipMemcpyHostToDevice, st);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(exp_init_keys, dim3(2048), dim3(256), 0, st, n, seg, B.keys, B.vals);
-    return hipGetLastError();
-}
-// after shade(b): sort queue b+1's slots by key and permute its streams
-hipError_t exp_sort_post(int h, uint32_t n, float4* q, uint32_t qs, hipStream_t st) {
-    ExpSortBufs& B = g_exp[h];
-    size_t tb = B.cub_bytes;
-    hipError_t e = hipcub::DeviceRadixSort::SortPairs(B.cub, tb, B.keys, B.keys2, B.vals, B.vals2, (int)n, 0, 27, st);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(exp_permute, dim3(4096), dim3(256), 0, st, n, qs, B.vals2, q, B.tmp);
-    hipLaunchKernelGGL(exp_copy_back, dim3(4096), dim3(256), 0, st, n, qs, B.tmp, q);
-    return hipGetLastError();
-}
-#endif
 
 template <int S, int BLOCK>
 hipError_t launch_extend_primary(const KernelParams& kp, const WfParams& wf, int grid, size_t lds, hipStream_t st) {
@@ -1076,10 +977,6 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams* wf_in, co
                     e = launch_extend<false, 8, kGlobalBlock>(kb, wf, (int)nseg, (size_t)8 * kGlobalBlock * 16 + 32,
                                                               bs);
                 if (e != hipSuccess) break;
-#if MCPT_WF_EXP_SORT
-                const bool exp_sort = !in_lds && !wf.sort && b + 1 < max_bounces;
-                if (exp_sort && (e = exp_sort_pre(h, nseg * wf.seg, wf.seg, bs)) != hipSuccess) break;
-#endif
                 if (wf.sort)
                     hipLaunchKernelGGL(wf_shade, dim3(nseg * per), dim3(kShadeBlock), 0, bs, kb, wf, per);
                 else if (in_lds && ns == 1)   // alone on the GPU: 16 waves per segment keep HBM busy
@@ -1089,10 +986,6 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams* wf_in, co
                 else
                     hipLaunchKernelGGL(wf_shade_slots<256>, dim3(nseg), dim3(256), 0, bs, kb, wf);
                 e = hipGetLastError();
-#if MCPT_WF_EXP_SORT
-                if (e == hipSuccess && exp_sort)
-                    e = exp_sort_post(h, nseg * wf.seg, wf.q[(b + 1) & 1], wf.slot_stride, bs);
-#endif
             }
             if (e != hipSuccess) break;
             hipLaunchKernelGGL(wf_accumulate, dim3((wf.nb + 255u) / 256u, ncb), dim3(256), 0, bs, kb, wf);
