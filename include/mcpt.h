@@ -107,7 +107,7 @@ typedef struct {
      * time; 0 = automatic (the measured defaults).
      * mcpt_plan_query reports the values a render would use. */
     int32_t wf_streams;         /* wavefront HIP streams 1..4 the batches rotate over; 0: scenes in
-                                   LDS 2 (3 for frames of >= 2^29 paths), global-memory scenes 4 */
+                                   LDS 2 (3 for frames of more than 2^29 paths), global-memory scenes 4 */
     int32_t wf_refill;          /* wavefront extend: ready lanes before a wave refills (1..64);
                                    0: 16 (LDS scenes), 8 (global-memory scenes) */
     int32_t wf_group_shift;     /* wavefront, global-memory scenes: paths are dealt to queue

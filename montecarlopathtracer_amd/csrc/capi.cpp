@@ -390,13 +390,15 @@ int clamp_i(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 // 4 x 2^26 10.93; C4 1024 spp: 1 x 2^28 6.14, 2 x 2^28 8.07, 3 x 2^27 8.17,
 // 4 x 2^27 8.28 G rays/s, means of 2-3 runs).  mcpt_render_params::wf_streams
 // (1..4) overrides; 1 = every batch on the caller's stream.
-// LDS scenes: 3 streams for frames of >= 2^29 paths (C2 after the id-only hit
-// records: 2 x 2^28 13.48 / 13.45, 3 x 2^27 13.65 / 13.56, 3 x 2^30/9 13.65 /
-// 13.59 G rays/s), 2 below (one rank's C2 share at N = 8, 2^27 paths: 35.4 ms
-// on 2 streams, 37.6 on 3)
+// LDS scenes: 3 streams for frames of more than 2^29 paths (C2 after the
+// id-only hit records: 2 x 2^28 13.48 / 13.45, 3 x 2^27 13.65 / 13.56,
+// 3 x 2^30/9 13.65 / 13.59 G rays/s), 2 up to 2^29 (one rank's C2 share at
+// N = 2, 2^29 paths: 136.1 ms on 2 x 2^27, 136.7 on 2 x 2^28, 143.3 on
+// 3 x 2^27 -- four batches on three streams leave one alone at the end; at
+// N = 8, 2^27 paths: 35.4 ms on 2 streams, 37.6 on 3)
 int wavefront_streams(const mcpt_scene& s, uint64_t work, const mcpt_render_params* p) {
     const int n = p->wf_streams > 0 ? p->wf_streams
-                                    : (s.gpu.node_boxes ? 4 : (work >= (uint64_t(1) << 29) ? 3 : 2));
+                                    : (s.gpu.node_boxes ? 4 : (work > (uint64_t(1) << 29) ? 3 : 2));
     return clamp_i(n, 1, mcpt::kMaxWfStreams);
 }
 
