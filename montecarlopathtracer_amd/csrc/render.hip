@@ -291,7 +291,7 @@ __global__ void __launch_bounds__(BLOCK, (!IN_LDS && COUNT) ? 4 : 1) path_kernel
             }
 #endif
             if (mode == kTrav) {
-                if (trav_iter<S, !IN_LDS, COUNT>(r, tris, nodes, leafs, st, BLOCK, spill, spill_stride, c MCPT_LU_ARG, pairs))
+                if (trav_iter<S, !IN_LDS, COUNT, IN_LDS>(r, tris, nodes, leafs, st, BLOCK, spill, spill_stride, c MCPT_LU_ARG, pairs))
                     mode = kReady;
             }
             const uint64_t trv = __ballot(mode == kTrav);

@@ -241,6 +241,24 @@ __device__ __forceinline__ void test_tri(RayState& r, const float4* __restrict__
     test_tri_v(r, tris[k], tris[k + 1], tris[k + 2], k);
 }
 
+// A triangle record read whole (16 B): the compiler would narrow reads whose .w
+// is unused to 12 B, and the LDS array serves a ds_read_b96 in 8 cycles, a
+// ds_read_b128 in 4 (MI355X_MICROARCH.md, LDS table).
+#ifndef MCPT_TRI_B128
+#define MCPT_TRI_B128 1
+#endif
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) f32x4 lds_f32x4;
+template <bool IN_LDS>
+__device__ __forceinline__ float4 ld_tri(const float4* __restrict__ p) {
+    if constexpr (IN_LDS && MCPT_TRI_B128) {     // (volatile: not narrowed)
+        const f32x4 v = *(const volatile lds_f32x4*)p;
+        return make_float4(v.x, v.y, v.z, v.w);
+    } else {
+        return *p;
+    }
+}
+
 // One resumable traversal iteration: descend to a leaf, test it (two
 // triangles at most, both records read up front), pop (the stack top read
 // during the tests).  Returns true when the ray's closest hit is final.  The
@@ -444,7 +462,9 @@ __device__ __forceinline__ int descend_steps(RayState& r, const uint2* __restric
 }
 
 // COUNT = false (lean renders): the counters below are compiled out (rays stay)
-template <int S, bool BOXES = false, bool COUNT = true>
+// TRIS_LDS: `tris` points into LDS (the scene image copied there), so its
+// records can be read by full-width LDS loads (ld_tri)
+template <int S, bool BOXES = false, bool COUNT = true, bool TRIS_LDS = false>
 __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict__ tris,
                                           const uint2* __restrict__ nodes1, const uint32_t* __restrict__ leafs,
                                           uint4* st, int stride, uint4* __restrict__ spill, uint32_t spill_stride,
@@ -471,8 +491,9 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
         const bool two = r.lend - r.lpos >= 2u;
         const uint32_t k0 = leafs[r.lpos], k1n = leafs[r.lpos + 1u];
         const uint32_t k1 = two ? k1n : k0;
-        const float4 a0 = tris[k0], a1 = tris[k0 + 1], a2 = tris[k0 + 2];
-        const float4 b0 = tris[k1], b1 = tris[k1 + 1], b2 = tris[k1 + 2];
+        const float4 a0 = ld_tri<TRIS_LDS>(tris + k0), a1 = ld_tri<TRIS_LDS>(tris + k0 + 1);
+        const float4 a2 = ld_tri<TRIS_LDS>(tris + k0 + 2), b0 = ld_tri<TRIS_LDS>(tris + k1);
+        const float4 b1 = ld_tri<TRIS_LDS>(tris + k1 + 1), b2 = ld_tri<TRIS_LDS>(tris + k1 + 2);
         MCPT_LANE_USE(tri_w, tri_l, lu);
         if constexpr (COUNT) c.refs += two ? 2u : 1u;
         if constexpr (COUNT) c.tests += two ? 2u : 1u;

@@ -364,7 +364,7 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
             }
 #endif
             if (mode == kTrav) {
-                if (trav_iter<S, !IN_LDS, COUNT>(r, tris, nodes, leafs, st, BLOCK, spill, spill_stride, c MCPT_LU_ARG,
+                if (trav_iter<S, !IN_LDS, COUNT, IN_LDS>(r, tris, nodes, leafs, st, BLOCK, spill, spill_stride, c MCPT_LU_ARG,
                                                  pairs))
                     mode = kReady;
             }
@@ -598,8 +598,9 @@ __global__ void __launch_bounds__(BLOCK) wf_extend_primary(const KernelParams kp
                         const bool two = lend - i >= 2u;
                         const uint32_t k0 = leafs[i], k1n = leafs[i + 1u];
                         const uint32_t k1 = two ? k1n : k0;
-                        const float4 a0 = tris[k0], a1 = tris[k0 + 1], a2 = tris[k0 + 2];
-                        const float4 b0 = tris[k1], b1 = tris[k1 + 1], b2 = tris[k1 + 2];
+                        const float4 a0 = ld_tri<true>(tris + k0), a1 = ld_tri<true>(tris + k0 + 1);
+                        const float4 a2 = ld_tri<true>(tris + k0 + 2), b0 = ld_tri<true>(tris + k1);
+                        const float4 b1 = ld_tri<true>(tris + k1 + 1), b2 = ld_tri<true>(tris + k1 + 2);
                         if (active) {
                             test_tri_pair(r, a0, a1, a2, k0, b0, b1, b2, k1, two);
                             if constexpr (COUNT) {
