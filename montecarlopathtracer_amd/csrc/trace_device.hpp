@@ -463,8 +463,9 @@ __device__ __forceinline__ int descend_steps(RayState& r, const uint2* __restric
 
 // COUNT = false (lean renders): the counters below are compiled out (rays stay)
 // TRIS_LDS: `tris` points into LDS (the scene image copied there), so its
-// records can be read by full-width LDS loads (ld_tri)
-template <int S, bool BOXES = false, bool COUNT = true, bool TRIS_LDS = false>
+// records can be read by full-width LDS loads (ld_tri).  CAP: descent steps per
+// call (0: MCPT_DESCENT_CAP / MCPT_DESCENT_CAP_GLOBAL).
+template <int S, bool BOXES = false, bool COUNT = true, bool TRIS_LDS = false, int CAP = 0>
 __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict__ tris,
                                           const uint2* __restrict__ nodes1, const uint32_t* __restrict__ leafs,
                                           uint4* st, int stride, uint4* __restrict__ spill, uint32_t spill_stride,
@@ -472,7 +473,8 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
     const int32_t U = stride * 16;            // one stack position (see slot_of)
     if (r.lpos == r.lend) {                   // between leaves: descend
         const int k = descend_steps<S, BOXES, COUNT>(r, nodes1, st, stride, spill, spill_stride, c, pairs,
-                                                      BOXES ? MCPT_DESCENT_CAP_GLOBAL : MCPT_DESCENT_CAP MCPT_LU_ARG);
+                                                      CAP > 0 ? CAP : BOXES ? MCPT_DESCENT_CAP_GLOBAL : MCPT_DESCENT_CAP
+                                                      MCPT_LU_ARG);
         if (k == 0) return false;
         if (k == 2) return true;
     }

@@ -262,6 +262,16 @@ struct ClassBuf {
 #define MCPT_WF_EXT_PRIO 0
 #endif
 
+// Descent steps per traversal call in the wavefront extend (the megakernel's
+// MCPT_DESCENT_CAP is 4): with shading out of the loop a longer descent burst
+// pays (C2 wf cap 3 / 4 / 5 / 6: 13.57 / 13.64 / 13.84 / 13.57 G rays/s)
+#ifndef MCPT_WF_DESCENT_CAP
+#define MCPT_WF_DESCENT_CAP 5
+#endif
+#ifndef MCPT_WF_DESCENT_CAP_GLOBAL
+#define MCPT_WF_DESCENT_CAP_GLOBAL MCPT_DESCENT_CAP_GLOBAL
+#endif
+
 // ---- extend: closest hit of every ray of this workgroup's segment -----------
 // COUNT = false (lean renders): the traversal counters are compiled out.
 // SORT = WfParams::sort, a template argument so that the queue-order variant
@@ -364,7 +374,7 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
             }
 #endif
             if (mode == kTrav) {
-                if (trav_iter<S, !IN_LDS, COUNT, IN_LDS>(r, tris, nodes, leafs, st, BLOCK, spill, spill_stride, c MCPT_LU_ARG,
+                if (trav_iter<S, !IN_LDS, COUNT, IN_LDS, IN_LDS ? MCPT_WF_DESCENT_CAP : MCPT_WF_DESCENT_CAP_GLOBAL>(r, tris, nodes, leafs, st, BLOCK, spill, spill_stride, c MCPT_LU_ARG,
                                                  pairs))
                     mode = kReady;
             }
