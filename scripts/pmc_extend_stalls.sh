@@ -1,6 +1,6 @@
 #!/bin/bash
 # Where the wavefront extend's wave cycles go (run on the GPU box via gpurun):
-# three SQ passes over one C2 render (bench.py --pmc-child), then a per-kernel
+# four SQ passes over one C2 render (bench.py --pmc-child), then a per-kernel
 # breakdown -- parked on s_waitcnt (WAIT_ANY), issue-stalled (WAIT_INST_ANY),
 # issuing (ACTIVE_INST_*), instruction mix per ray.  ARGS adds workload flags.
 set -e
@@ -17,5 +17,6 @@ pass() {   # name counters...
 pass stall SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_WAIT_INST_LDS
 pass mix SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM SQ_THREAD_CYCLES_VALU SQ_BUSY_CYCLES
 pass misc SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_VMEM SQ_INSTS_SMEM SQ_WAVES GRBM_GUI_ACTIVE
+pass lds SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS GRBM_COUNT
 cd $R
 python3 scripts/stall_summary.py $O

@@ -10,6 +10,7 @@ import json
 import os
 import sys
 
+CUS = 256
 KINDS = (("wf_extend_primary", "extend_bounce0"), ("wf_extend<", "extend"), ("wf_shade", "shade"),
          ("wf_generate", "generate"))
 
@@ -21,14 +22,17 @@ def kind(name):
 
 
 def main(d):
-    acc, ns = {}, {}
-    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+    acc, ns, src = {}, {}, {}
+    for f in sorted(glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)):
         for row in csv.DictReader(open(f)):
             k = kind(row.get("Kernel_Name", ""))
             if k is None:
                 continue
+            cn = row["Counter_Name"]
+            if src.setdefault(cn, f) != f:   # a counter collected in two passes: count one
+                continue
             c = acc.setdefault(k, {})
-            c[row["Counter_Name"]] = c.get(row["Counter_Name"], 0.0) + float(row["Counter_Value"])
+            c[cn] = c.get(cn, 0.0) + float(row["Counter_Value"])
             if row["Counter_Name"] == "SQ_WAVE_CYCLES":
                 ns.setdefault(k, {})[row["Dispatch_Id"]] = int(row["End_Timestamp"]) - int(row["Start_Timestamp"])
     out = {}
@@ -49,6 +53,10 @@ def main(d):
             r["lane_use_per_valu_inst"] = round(c["SQ_THREAD_CYCLES_VALU"] / 64.0 / c["SQ_INSTS_VALU"], 4)
         if c.get("SQ_LDS_BANK_CONFLICT") and c.get("SQ_INSTS_LDS"):
             r["lds_conflict_cycles_per_lds_inst"] = round(c["SQ_LDS_BANK_CONFLICT"] / c["SQ_INSTS_LDS"], 3)
+        if c.get("SQ_LDS_IDX_ACTIVE") and c.get("GRBM_GUI_ACTIVE"):
+            # LDS-array cycles summed over CUs / (CUs x kernel cycles); GRBM_GUI_ACTIVE is summed over 8 XCDs
+            r["lds_idx_active_G"] = round(c["SQ_LDS_IDX_ACTIVE"] / 1e9, 3)
+            r["lds_array_busy"] = round(c["SQ_LDS_IDX_ACTIVE"] / CUS / (c["GRBM_GUI_ACTIVE"] / 8), 4)
         if c.get("GRBM_GUI_ACTIVE") and r["ms"]:
             r["clock_GHz"] = round(c["GRBM_GUI_ACTIVE"] / 8 / (r["ms"] * 1e6), 3)
         out[k] = r
