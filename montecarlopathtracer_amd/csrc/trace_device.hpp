@@ -115,18 +115,19 @@ __device__ __forceinline__ bool begin_ray(RayState& r, const GpuScene& sc, float
     float tmin = 0.0f, tmax = kFltMax;
     const float oo[3] = {r.o.x, r.o.y, r.o.z}, dd[3] = {r.d.x, r.d.y, r.d.z}, inv[3] = {r.ix, r.iy, r.iz};
     bool miss = false;
+    // branch-free: a zero direction component only tests the origin against
+    // that slab and leaves the interval alone (no exec-mask branches in the
+    // extend's hand-off, where every new ray passes through here)
 #pragma unroll
     for (int a = 0; a < 3; a++) {
-        if (dd[a] == 0.0f) {
-            miss = miss || (oo[a] < sc.root_min[a] || oo[a] > sc.root_max[a]);
-        } else {
-            const float t0 = (sc.root_min[a] - oo[a]) * inv[a];
-            const float t1 = (sc.root_max[a] - oo[a]) * inv[a];
-            const float lo = dd[a] < 0.0f ? t1 : t0;
-            const float hi = dd[a] < 0.0f ? t0 : t1;
-            tmin = lo > tmin ? lo : tmin;
-            tmax = hi < tmax ? hi : tmax;
-        }
+        const bool z = dd[a] == 0.0f;
+        miss = miss | (z & ((oo[a] < sc.root_min[a]) | (oo[a] > sc.root_max[a])));
+        const float t0 = (sc.root_min[a] - oo[a]) * inv[a];
+        const float t1 = (sc.root_max[a] - oo[a]) * inv[a];
+        const float lo = dd[a] < 0.0f ? t1 : t0;
+        const float hi = dd[a] < 0.0f ? t0 : t1;
+        tmin = (!z & (lo > tmin)) ? lo : tmin;
+        tmax = (!z & (hi < tmax)) ? hi : tmax;
     }
     r.tmin = tmin;
     // the walk compares against tmax only as tmax * kEpsHi, so the state keeps
