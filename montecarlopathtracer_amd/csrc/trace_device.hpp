@@ -671,6 +671,11 @@ __device__ __forceinline__ uint32_t material_class(const GpuGeom& g) {
 // ---- wave-level helpers -----------------------------------------------------
 // Reserve one slot per lane with `want` in a device-wide append buffer: one
 // atomic per wave (ballot + popcount), lanes ranked by their position.
+// x of lane `src` (wave-uniform) for every lane: v_readlane into a scalar
+// register -- what __shfl(x, src) computes, without its ds_bpermute round trip
+__device__ __forceinline__ uint32_t lane_bcast(uint32_t x, int src) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, src);
+}
 __device__ __forceinline__ uint32_t wave_append(bool want, uint32_t* counter) {
     const uint64_t m = __ballot(want);
     const int lane = (int)(threadIdx.x & 63u);
@@ -678,7 +683,7 @@ __device__ __forceinline__ uint32_t wave_append(bool want, uint32_t* counter) {
     if (m) {
         const int leader = __ffsll((unsigned long long)m) - 1;
         if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
-        base = __shfl(base, leader);
+        base = lane_bcast(base, leader);
     }
     return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
 }
@@ -698,7 +703,7 @@ struct SlotCursor {
             const uint32_t first = kChunk - used;
             uint32_t nb = 0;
             if (lane == 0) nb = atomicAdd(counter, kChunk);
-            nb = __shfl(nb, 0);
+            nb = lane_bcast(nb, 0);
             if (rank >= first) res = nb + (rank - first);
             base = nb;
             used = n - first;

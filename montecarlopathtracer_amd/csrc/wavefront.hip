@@ -239,7 +239,7 @@ struct ClassBuf {
             if (mine && (uint32_t)lane >= count) val = recv;
             uint32_t b = 0;
             if (lane == 0) b = atomicAdd(counter, kChunk);
-            b = __shfl(b, 0);
+            b = lane_bcast(b, 0);
             list[b + (uint32_t)lane] = val;
             if (mine && (uint32_t)lane < count) val = recv;
             count = hi - kChunk;
@@ -250,7 +250,7 @@ struct ClassBuf {
         const int lane = (int)(threadIdx.x & 63u);
         uint32_t b = 0;
         if (lane == 0) b = atomicAdd(counter, count);
-        b = __shfl(b, 0);
+        b = lane_bcast(b, 0);
         if ((uint32_t)lane < count) list[b + (uint32_t)lane] = val;
         count = 0;
     }
@@ -341,12 +341,10 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
         r.o = v3(opaque(o4.x), opaque(o4.y), opaque(o4.z));
         r.d = v3(opaque(d4.x), opaque(d4.y), opaque(d4.z));
         depth = __float_as_uint(d4.w);
-        if (depth == kNoRay) {
-            r.htri = -1;
-            mode = kReady;
-        } else {
-            mode = begin_ray(r, sc, kp.best_init) ? kTrav : kReady;
-        }
+        // (no branch: an empty slot's walk is set up and dropped; begin_ray
+        // leaves htri = -1, its miss)
+        const bool live = begin_ray(r, sc, kp.best_init);
+        mode = (depth != kNoRay && live) ? kTrav : kReady;
     };
 #ifdef MCPT_PHASE_TIMING
     // stats[8] setup, [9] traversal bursts, [10] hand-offs, [11] burst iterations
@@ -404,12 +402,11 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
                 const GpuGeom& gm = geoms[__float_as_uint(tris[r.htri + 1].w)];
                 if (!is_emitter(gm)) cls = material_class(gm);
             }
-            if (nslot < count) {
-                slot = nslot;
-                start(no4, nd4);
-            } else {
-                mode = kDead;
-            }
+            // (the next ray set up unconditionally: no branch in the hand-off; a
+            // lane past the segment's end runs on its stale prefetch, then dies)
+            slot = nslot;
+            start(no4, nd4);
+            if (nslot >= count) mode = kDead;
             if constexpr (MCPT_WF_HIT_ID && !SORT)   // (r holds the next ray by now: the id from hrec)
                 reinterpret_cast<int32_t*>(qb + qf(0, 2, qs))[seg0 + fslot] = __float_as_int(hrec.w);
             else if constexpr ((MCPT_WF_NT & 4) != 0 || (!IN_LDS && MCPT_WF_NT_HIT_GLOBAL))
@@ -521,7 +518,7 @@ __global__ void __launch_bounds__(BLOCK) wf_extend_primary(const KernelParams kp
     for (;;) {
         uint32_t grp = 0;
         if (lane == 0) grp = atomicAdd(lgrp, 1u);
-        const uint32_t base = uni((uint32_t)__shfl((int)grp, 0)) << 6;   // this wave's 64-slot group
+        const uint32_t base = lane_bcast(grp, 0) << 6;   // this wave's 64-slot group
         if (base >= count) break;
         const uint32_t slot = base + (uint32_t)lane;
         RayState r;
@@ -840,7 +837,7 @@ __global__ void __launch_bounds__(BLOCK) wf_shade_slots(const KernelParams kp, c
             const int leader = __ffsll((unsigned long long)m) - 1;
             uint32_t b0 = 0;
             if (lane == leader) b0 = atomicAdd(&lnext, (uint32_t)__popcll(m));
-            b0 = __shfl(b0, leader);
+            b0 = lane_bcast(b0, leader);
             if (cont) {
                 const size_t ji = seg0 + b0 + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
                 stq(&qb2[qf(ji, 0, qs)], pack(o, pid));
