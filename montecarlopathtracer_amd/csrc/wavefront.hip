@@ -386,7 +386,11 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
         // Settle the prefetch (issued a whole burst ago) before any store of
         // this hand-off: gfx9's vmcnt also counts stores, so any later wait on
         // the prefetch registers would wait for the stores' acknowledgements.
-        no4 = make_float4(opaque(no4.x), opaque(no4.y), opaque(no4.z), no4.w);
+        // The origin's .w (unused here) is settled too: it keeps its register
+        // live across the burst -- a dead load destination is reused by the
+        // loop, which must then wait for the load first (a vmcnt wait in every
+        // burst's first iteration: C2 +0.9%, C4 +2.8% without it).
+        no4 = make_float4(opaque(no4.x), opaque(no4.y), opaque(no4.z), opaque(no4.w));
         nd4 = make_float4(opaque(nd4.x), opaque(nd4.y), opaque(nd4.z), opaque(nd4.w));
         const bool fin = mode == kReady;
         uint32_t cls = 4u;
