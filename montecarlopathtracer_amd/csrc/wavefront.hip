@@ -519,23 +519,37 @@ __global__ void __launch_bounds__(BLOCK) wf_extend_primary(const KernelParams kp
     const V3 eye = v3(kp.eye[0], kp.eye[1], kp.eye[2]);
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0};
     __builtin_amdgcn_s_setprio(MCPT_WF_EXT_PRIO);
-    for (;;) {
+    // a wave's 64-slot groups: the next group is taken, and its directions
+    // loaded, before this one's walk, so the load's latency hides behind it
+    auto take_group = [&]() {
         uint32_t grp = 0;
         if (lane == 0) grp = atomicAdd(lgrp, 1u);
-        const uint32_t base = lane_bcast(grp, 0) << 6;   // this wave's 64-slot group
+        return lane_bcast(grp, 0) << 6;
+    };
+    // The hits of a group are stored one group later, after the wait for the
+    // next directions: a store issued at the end of the walk would make that
+    // wait (vmcnt counts stores too) wait for its acknowledgement.
+    int32_t* const hq = reinterpret_cast<int32_t*>(qb + qf(0, 2, qs)) + seg0;
+    uint32_t base = take_group();
+    float4 nd4 = make_float4(0, 0, 0, 0);
+    if (base + (uint32_t)lane < count) nd4 = ldq(&qb[qf(seg0 + base + (uint32_t)lane, 1, qs)]);
+    uint32_t pslot = count;                             // the previous group's slot (count: none)
+    int32_t phit = -1;
+    for (;;) {
         if (base >= count) break;
         const uint32_t slot = base + (uint32_t)lane;
+        const float4 d4 = make_float4(opaque(nd4.x), opaque(nd4.y), opaque(nd4.z), opaque(nd4.w));
+        if (pslot < count) hq[pslot] = phit;
+        const uint32_t nbase = take_group();
+        if (nbase + (uint32_t)lane < count) nd4 = ldq(&qb[qf(seg0 + nbase + (uint32_t)lane, 1, qs)]);
         RayState r;
         r.o = eye;
         r.d = v3(0, 0, 1);
         r.htri = -1;
         bool active = false, done = false;
-        if (slot < count) {
-            const float4 d4 = ldq(&qb[qf(seg0 + slot, 1, qs)]);
-            if (__float_as_uint(d4.w) != kNoRay) {
-                r.d = xyz(d4);
-                active = begin_ray(r, sc, kp.best_init);
-            }
+        if (slot < count && __float_as_uint(d4.w) != kNoRay) {
+            r.d = xyz(d4);
+            active = begin_ray(r, sc, kp.best_init);
         }
         uint32_t w0 = sc.root_w[0], w1 = sc.root_w[1];  // the wave's node
         int32_t sp = 0, lo = 0;                         // wave-uniform stack positions
@@ -653,8 +667,11 @@ __global__ void __launch_bounds__(BLOCK) wf_extend_primary(const KernelParams kp
                 if (!more) break;
             }
         }
-        if (slot < count) reinterpret_cast<int32_t*>(qb + qf(0, 2, qs))[seg0 + slot] = r.htri;
+        pslot = slot;
+        phit = r.htri;
+        base = nbase;
     }
+    if (pslot < count) hq[pslot] = phit;
     flush_counters(c, kp.stats);
     __syncthreads();
     if (tid < 4) cn->cls[tid] = 0;
