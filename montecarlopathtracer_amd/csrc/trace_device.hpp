@@ -217,6 +217,10 @@ __device__ __forceinline__ void test_tri_v(RayState& r, const float4 A0, const f
 #ifndef MCPT_TAIL_MERGE
 #define MCPT_TAIL_MERGE 1
 #endif
+// EARLY_PRIO (records in global memory): the tail's rank select is made before
+// the tail's branch, so the records' .w words come with their first loads
+// (one 16-B load each) instead of a dependent 4-B load inside the tail
+template <bool EARLY_PRIO = false>
 __device__ __forceinline__ void test_tri_pair(RayState& r, const float4 A0, const float4 A1, const float4 A2,
                                               uint32_t ka, const float4 B0, const float4 B1, const float4 B2,
                                               uint32_t kb, bool two) {
@@ -224,13 +228,16 @@ __device__ __forceinline__ void test_tri_pair(RayState& r, const float4 A0, cons
     const bool oka = tri_prefilter(r, A0, A1, A2, qa);
     const bool okb = tri_prefilter(r, B0, B1, B2, qb) & two;
 #if MCPT_TAIL_MERGE
+    uint32_t prio = 0;
+    if constexpr (EARLY_PRIO) prio = oka ? __float_as_uint(A0.w) : __float_as_uint(B0.w);
     if (oka | okb) {
         TriDets q;
         q.detA = oka ? qa.detA : qb.detA;
         q.qb = oka ? qa.qb : qb.qb;
         q.qg = oka ? qa.qg : qb.qg;
         q.qt = oka ? qa.qt : qb.qt;
-        tri_accept(r, q, oka ? __float_as_uint(A0.w) : __float_as_uint(B0.w), oka ? ka : kb);
+        if constexpr (!EARLY_PRIO) prio = oka ? __float_as_uint(A0.w) : __float_as_uint(B0.w);
+        tri_accept(r, q, prio, oka ? ka : kb);
     }
     if (oka & okb) tri_accept(r, qb, __float_as_uint(B0.w), kb);
 #else
@@ -500,7 +507,7 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
         MCPT_LANE_USE(tri_w, tri_l, lu);
         if constexpr (COUNT) c.refs += two ? 2u : 1u;
         if constexpr (COUNT) c.tests += two ? 2u : 1u;
-        test_tri_pair(r, a0, a1, a2, k0, b0, b1, b2, k1, two);
+        test_tri_pair<!TRIS_LDS>(r, a0, a1, a2, k0, b0, b1, b2, k1, two);
         r.lpos += two ? 2u : 1u;
     }
     if (r.lpos < r.lend) return false;        // more triangles in this leaf
