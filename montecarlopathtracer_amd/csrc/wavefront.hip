@@ -272,6 +272,11 @@ struct ClassBuf {
 #define MCPT_WF_DESCENT_CAP_GLOBAL MCPT_DESCENT_CAP_GLOBAL
 #endif
 
+#ifndef MCPT_WF_GEO_LDS
+#define MCPT_WF_GEO_LDS 1
+#endif
+constexpr size_t kLdsPerCu = 160 * 1024;
+
 // ---- extend: closest hit of every ray of this workgroup's segment -----------
 // COUNT = false (lean renders): the traversal counters are compiled out.
 // SORT = WfParams::sort, a template argument so that the queue-order variant
@@ -758,19 +763,28 @@ __global__ void __launch_bounds__(kShadeBlock) wf_shade(const KernelParams kp, c
 // continuing ray goes to the next free slot of the segment's queue b+1 (one
 // LDS atomic per wave, 64 consecutive slots), so queue b+1 is dense.  Queue
 // order is scheduling-dependent, but nothing reads it (state keyed by pid).
-template <int BLOCK>
+template <int BLOCK, bool GEO_LDS>
 __global__ void __launch_bounds__(BLOCK) wf_shade_slots(const KernelParams kp, const WfParams wf) {
     const uint32_t g = blockIdx.x;
     if (g >= wf.nseg) return;
     __shared__ uint32_t lnext;
+    // the material table in LDS when it fits beside the co-resident extend
+    // (GEO_LDS): its fields are read in the branches of the shading chain,
+    // each a dependent round trip that LDS serves in a fraction of L2's time
+    extern __shared__ GpuGeom lgeo[];
     const WfCounters* cn = wf.cnt + (size_t)wf.bounce * wf.nseg + g;
     WfCounters* nx = wf.cnt + (size_t)(wf.bounce + 1) * wf.nseg + g;
     const uint32_t total = cn->queued;
-    if (threadIdx.x == 0) lnext = 0;
-    __syncthreads();
     const GpuScene& sc = kp.scene;
+    if (threadIdx.x == 0) lnext = 0;
+    if constexpr (GEO_LDS) {
+        const uint4* src = reinterpret_cast<const uint4*>(sc.image + sc.off_geoms);
+        uint4* dst = reinterpret_cast<uint4*>(lgeo);
+        for (uint32_t i = threadIdx.x; i < sc.n_geoms * 4u; i += BLOCK) dst[i] = src[i];
+    }
+    __syncthreads();
     const float4* tris = reinterpret_cast<const float4*>(sc.image + sc.off_tris);
-    const GpuGeom* geoms = reinterpret_cast<const GpuGeom*>(sc.image + sc.off_geoms);
+    const GpuGeom* geoms = GEO_LDS ? lgeo : reinterpret_cast<const GpuGeom*>(sc.image + sc.off_geoms);
     const size_t seg0 = (size_t)g * wf.seg;
     const float4* qb = wf.q[wf.bounce & 1];
     float4* qb2 = wf.q[(wf.bounce + 1) & 1];
@@ -895,6 +909,9 @@ hipError_t launch_extend_primary(const KernelParams& kp, const WfParams& wf, int
     return hipGetLastError();
 }
 
+template <int BLOCK>
+auto shade_kernel(bool geo_lds) { return geo_lds ? wf_shade_slots<BLOCK, true> : wf_shade_slots<BLOCK, false>; }
+
 template <bool IN_LDS, int S, int BLOCK>
 hipError_t launch_extend(const KernelParams& kp, const WfParams& wf, int grid, size_t lds, hipStream_t st) {
     auto kern = wf.sort ? (kp.lean ? wf_extend<IN_LDS, S, BLOCK, false, true> : wf_extend<IN_LDS, S, BLOCK, true, true>)
@@ -981,6 +998,12 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams* wf_in, co
             wf.v0 = v0;
             wf.nb = (kp.npix_local - v0) < nb_max ? (kp.npix_local - v0) : nb_max;
             const uint32_t n = wf.nb * wf.ns;
+            // the shade's material table in LDS if it fits beside the extend's
+            // workgroups on a CU (MCPT_WF_GEO_LDS)
+            const size_t ext_lds = in_lds ? lds_bytes_in_lds(img, 4) + 32
+                                          : (size_t)kGlobalBlocksPerCu * (8 * kGlobalBlock * 16 + 32);
+            const size_t geo_bytes = (MCPT_WF_GEO_LDS && ext_lds + 64 * (size_t)kp.scene.n_geoms + 64 <= kLdsPerCu)
+                                         ? 64 * (size_t)kp.scene.n_geoms : 0;
             // LDS scenes: one 8x8 tile of one sample per group; global-memory
             // scenes: the planned group size (whole image regions per segment)
             wf.group_shift = in_lds ? 6u : wf_in[h].group_shift;
@@ -1009,11 +1032,11 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams* wf_in, co
                 if (wf.sort)
                     hipLaunchKernelGGL(wf_shade, dim3(nseg * per), dim3(kShadeBlock), 0, bs, kb, wf, per);
                 else if (in_lds && ns == 1)   // alone on the GPU: 16 waves per segment keep HBM busy
-                    hipLaunchKernelGGL(wf_shade_slots<1024>, dim3(nseg), dim3(1024), 0, bs, kb, wf);
+                    hipLaunchKernelGGL(shade_kernel<1024>(geo_bytes != 0), dim3(nseg), dim3(1024), geo_bytes, bs, kb, wf);
                 else if (in_lds)              // beside an extend workgroup: 8 waves (2 x 64 VGPRs per SIMD)
-                    hipLaunchKernelGGL(wf_shade_slots<512>, dim3(nseg), dim3(512), 0, bs, kb, wf);
+                    hipLaunchKernelGGL(shade_kernel<512>(geo_bytes != 0), dim3(nseg), dim3(512), geo_bytes, bs, kb, wf);
                 else
-                    hipLaunchKernelGGL(wf_shade_slots<256>, dim3(nseg), dim3(256), 0, bs, kb, wf);
+                    hipLaunchKernelGGL(shade_kernel<256>(geo_bytes != 0), dim3(nseg), dim3(256), geo_bytes, bs, kb, wf);
                 e = hipGetLastError();
             }
             if (e != hipSuccess) break;
