@@ -332,6 +332,12 @@ __device__ __forceinline__ bool box_hit(const RayState& r, uint32_t b0, uint32_t
     return !out && !(lo * kEpsLo > hi * kEpsHi);
 }
 
+// a loaded value made an asm output: its wait sits here, not at a later join
+__device__ __forceinline__ uint4 settle4(uint4 v) {
+    asm volatile("v_mov_b32 %0, %0\n\tv_mov_b32 %1, %1\n\tv_mov_b32 %2, %2\n\tv_mov_b32 %3, %3"
+                 : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
+    return v;
+}
 // Pop the next interval: false = traversal finished (empty stack, or the best
 // hit lies before the popped interval)
 // LAZY (scenes in LDS, 4-entry LDS part): the LDS part holds entries
@@ -351,7 +357,10 @@ __device__ __forceinline__ bool pop_entry(RayState& r, uint4* st, int stride, ui
     uint4 e;
     if constexpr (LAZY) {
         if (r.sp < r.lo) {                    // LDS part empty: the entry is in memory
-            e = spill[((uint32_t)r.sp / (uint32_t)U) * spill_stride];
+            // (settled inside this branch: at the join a wait for it would be
+            // a vmcnt(0) on every pop, i.e. a wait for the extend's next-ray
+            // prefetch and hit stores)
+            e = settle4(spill[((uint32_t)r.sp / (uint32_t)U) * spill_stride]);
             r.lo = r.sp;
         } else {
             if (top) e = *top;

@@ -358,6 +358,11 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
 #else
 #define WF_STAMP(acc) do {} while (0)
 #endif
+    // the refill threshold as an asm result: a kernel argument read in the
+    // loop was a scalar load still counted at the loop's exit test, whose
+    // lgkmcnt(0) then also waited for every LDS access in flight, each iteration
+    int refill;
+    asm volatile("s_mov_b32 %0, %1" : "=s"(refill) : "s"(wf.refill_thresh));
     // MCPT_WF_IMPLICIT0 >= 2: bounce 0's origins are the eye (CV mode), not read
     const bool eye0 = MCPT_WF_IMPLICIT0 >= 2 && wf.bounce == 0 && implicit0(kp, wf);
     const float4 eye4 = make_float4(kp.eye[0], kp.eye[1], kp.eye[2], 0.0f);
@@ -383,7 +388,7 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
             }
             const uint64_t trv = __ballot(mode == kTrav);
             const uint64_t rdy = __ballot(mode == kReady);
-            if (!trv || (int)__popcll(rdy) >= wf.refill_thresh) break;
+            if (!trv || (int)__popcll(rdy) >= refill) break;
         }
         WF_STAMP(tm_trav);
         // ---- hand-off: hit record + per-material class list -----------------
@@ -646,7 +651,7 @@ __global__ void __launch_bounds__(BLOCK) wf_extend_primary(const KernelParams kp
                     sp -= U;
                     uint4 e;
                     if (sp < lo) {                               // LDS part empty: the entry is in memory
-                        e = spill[((uint32_t)sp / (uint32_t)U) * spill_stride];
+                        e = settle4(spill[((uint32_t)sp / (uint32_t)U) * spill_stride]);   // (wait here)
                         lo = sp;
                     } else {
                         e = ld4(slot_of<S>(st, BLOCK, sp));
