@@ -141,6 +141,22 @@ __device__ __forceinline__ uint32_t slot_pid(const WfParams& wf, uint32_t g, uin
     return ((blk * wf.nseg + k) << gs) | (j & ((1u << gs) - 1u));
 }
 
+// Length of segment g's queue 0 for the batch: its whole groups (the last
+// group of the batch may be partial).  Written by generate, or by the
+// generate-free bounce-0 extend (MCPT_WF_GEN0).
+__device__ __forceinline__ uint32_t seg_queue0_len(const WfParams& wf, uint32_t g) {
+    const uint32_t n = wf.nb * wf.ns;
+    const uint32_t gs = wf.group_shift, gm = (1u << gs) - 1u;
+    const uint32_t ngroups = (n + gm) >> gs;
+    const uint32_t full = ngroups / wf.nseg, rem = ngroups - full * wf.nseg;
+    // block `full` (partial, rem groups) covers segments rot, rot+1, ... (mod nseg)
+    const uint32_t k = (g + wf.nseg - seg_of(0, full, wf.nseg)) % wf.nseg;
+    uint32_t len = (full + (k < rem ? 1u : 0u)) << gs;
+    const uint32_t lb = (ngroups - 1u) / wf.nseg;            // block of the last group
+    if (seg_of(ngroups - 1u - lb * wf.nseg, lb, wf.nseg) == g) len -= (ngroups << gs) - n;
+    return len;
+}
+
 // MCPT_WF_IMPLICIT0 = 1: bounce 0's shade (queue order, CV mode) recomputes a
 // primary ray's origin, direction and RNG state from its slot instead of
 // reading them, and generate skips the {throughput, rng} stream (64 B of
@@ -172,7 +188,6 @@ static_assert(MCPT_WF_SOA || !MCPT_WF_HIT_ID, "hit ids use the SoA hit stream");
 __global__ void __launch_bounds__(kGenBlock) wf_generate(const KernelParams kp, const WfParams wf) {
     const uint32_t n = wf.nb * wf.ns;
     const uint32_t gs = wf.group_shift, gm = (1u << gs) - 1u;
-    const uint32_t ngroups = (n + gm) >> gs;
     const V3 eye = v3(kp.eye[0], kp.eye[1], kp.eye[2]);
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0};
     for (uint32_t pid = blockIdx.x * kGenBlock + threadIdx.x; pid < n; pid += gridDim.x * kGenBlock) {
@@ -181,15 +196,7 @@ __global__ void __launch_bounds__(kGenBlock) wf_generate(const KernelParams kp, 
         const uint32_t grp = pid >> gs, blk = grp / wf.nseg;
         const uint32_t g = seg_of(grp - blk * wf.nseg, blk, wf.nseg);
         const uint32_t slot = g * wf.seg + (blk << gs) + (pid & gm);
-        if (grp < wf.nseg && (pid & gm) == 0u) {    // segment g's queue length
-            const uint32_t full = ngroups / wf.nseg, rem = ngroups - full * wf.nseg;
-            // block `full` (partial, rem groups) covers segments rot, rot+1, ... (mod nseg)
-            const uint32_t k = (g + wf.nseg - seg_of(0, full, wf.nseg)) % wf.nseg;
-            uint32_t len = (full + (k < rem ? 1u : 0u)) << gs;
-            const uint32_t lb = (ngroups - 1u) / wf.nseg;            // block of the last group
-            if (seg_of(ngroups - 1u - lb * wf.nseg, lb, wf.nseg) == g) len -= (ngroups << gs) - n;
-            wf.cnt[g].queued = len;
-        }
+        if (grp < wf.nseg && (pid & gm) == 0u) wf.cnt[g].queued = seg_queue0_len(wf, g);   // segment g's queue length
         int px, py;
         V3 d = v3(0, 0, 0);
         uint32_t depth = kNoRay;
@@ -491,13 +498,30 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
 #endif
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
 
+// MCPT_WF_GEN0 (default 1): no generate kernel before this extend -- each
+// lane computes its slot's primary ray itself (the inverse dealing slot_pid
+// and primary_ray, as bounce 0's shade already does), writes the segment's
+// queue length and counts the paths; queue 0 holds no direction stream.
+// Generate was the only kernel of a frame's start (0.9 ms of one rank's 33 ms
+// share at N = 8) and moved 16 B per path through HBM twice.
+#ifndef MCPT_WF_GEN0
+#define MCPT_WF_GEN0 1
+#endif
 template <int S, int BLOCK, bool COUNT>
 __global__ void __launch_bounds__(BLOCK) wf_extend_primary(const KernelParams kp, const WfParams wf) {
     static_assert((BLOCK & (BLOCK - 1)) == 0, "stack slot addresses (slot_of) mask by a power-of-two block");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t g = blockIdx.x;
     WfCounters* cn = wf.cnt + (size_t)wf.bounce * wf.nseg + g;
-    const uint32_t count = g < wf.nseg ? cn->queued : 0u;
+    uint32_t count = 0;
+    if (g < wf.nseg) {
+        if constexpr (MCPT_WF_GEN0) {
+            count = seg_queue0_len(wf, g);
+            if (threadIdx.x == 0) cn->queued = count;          // (read by bounce 0's shade)
+        } else {
+            count = cn->queued;
+        }
+    }
     if (count == 0) {
         if (g < wf.nseg && threadIdx.x < 4) cn->cls[threadIdx.x] = 0;
         return;
@@ -540,9 +564,30 @@ __global__ void __launch_bounds__(BLOCK) wf_extend_primary(const KernelParams kp
     // next directions: a store issued at the end of the walk would make that
     // wait (vmcnt counts stores too) wait for its acknowledgement.
     int32_t* const hq = reinterpret_cast<int32_t*>(qb + qf(0, 2, qs)) + seg0;
+    // the primary ray of local slot j: direction and depth (kNoRay: a pixel
+    // outside the image, an empty slot)
+    auto dir_of = [&](uint32_t j) {
+        if constexpr (MCPT_WF_GEN0) {
+            const uint32_t pid = slot_pid(wf, g, j);
+            const uint32_t s_local = pid / wf.nb;
+            int px, py;
+            float4 d4 = make_float4(0, 0, 0, __uint_as_float(kNoRay));
+            if (unit_pixel(kp, wf.v0 + (pid - s_local * wf.nb), px, py)) {
+                uint32_t sd;
+                V3 d;
+                primary_ray(kp, (uint32_t)py * (uint32_t)kp.width + (uint32_t)px, px, py, wf.s_begin + s_local, sd, d);
+                d4 = pack(d, 0u);
+                c.paths++;                                      // (generate's counts)
+                c.rays++;
+            }
+            return d4;
+        } else {
+            return ldq(&qb[qf(seg0 + j, 1, qs)]);
+        }
+    };
     uint32_t base = take_group();
     float4 nd4 = make_float4(0, 0, 0, 0);
-    if (base + (uint32_t)lane < count) nd4 = ldq(&qb[qf(seg0 + base + (uint32_t)lane, 1, qs)]);
+    if (base + (uint32_t)lane < count) nd4 = dir_of(base + (uint32_t)lane);
     uint32_t pslot = count;                             // the previous group's slot (count: none)
     int32_t phit = -1;
     for (;;) {
@@ -551,7 +596,7 @@ __global__ void __launch_bounds__(BLOCK) wf_extend_primary(const KernelParams kp
         const float4 d4 = make_float4(opaque(nd4.x), opaque(nd4.y), opaque(nd4.z), opaque(nd4.w));
         if (pslot < count) hq[pslot] = phit;
         const uint32_t nbase = take_group();
-        if (nbase + (uint32_t)lane < count) nd4 = ldq(&qb[qf(seg0 + nbase + (uint32_t)lane, 1, qs)]);
+        if (nbase + (uint32_t)lane < count) nd4 = dir_of(nbase + (uint32_t)lane);
         RayState r;
         r.o = eye;
         r.d = v3(0, 0, 1);
@@ -1016,17 +1061,20 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams* wf_in, co
             wf.seg = ((((n + (1u << wf.group_shift) - 1u) >> wf.group_shift) + nseg - 1) / nseg) << wf.group_shift;
             e = hipMemsetAsync(wf.cnt, 0, sizeof(WfCounters) * (size_t)nseg * (size_t)(max_bounces + 1), bs);
             if (e != hipSuccess) break;
-            const uint32_t gen_grid = (n + kGenBlock - 1) / kGenBlock;
-            hipLaunchKernelGGL(wf_generate, dim3(gen_grid < 16u * (uint32_t)cus ? gen_grid : 16u * (uint32_t)cus),
-                               dim3(kGenBlock), 0, bs, kb, wf);
-            if ((e = hipGetLastError()) != hipSuccess) break;
+            // bounce 0 of CV mode (implicit queue 0: every origin is the eye): the
+            // wave-coherent extend, one tree walk per 64-ray tile (MCPT_WF_PACKET0),
+            // which also generates the primary rays (MCPT_WF_GEN0)
+            const bool packet = MCPT_WF_PACKET0 && in_lds && MCPT_WF_IMPLICIT0 >= 2 && implicit0(kb, wf) &&
+                                wf.group_shift == 6u;
+            if (!(packet && MCPT_WF_GEN0)) {
+                const uint32_t gen_grid = (n + kGenBlock - 1) / kGenBlock;
+                hipLaunchKernelGGL(wf_generate, dim3(gen_grid < 16u * (uint32_t)cus ? gen_grid : 16u * (uint32_t)cus),
+                                   dim3(kGenBlock), 0, bs, kb, wf);
+                if ((e = hipGetLastError()) != hipSuccess) break;
+            }
             for (int b = 0; b < max_bounces && e == hipSuccess; b++) {
                 wf.bounce = b;
-                // bounce 0 of CV mode (implicit queue 0: every origin is the eye): the
-                // wave-coherent extend, one tree walk per 64-ray tile (MCPT_WF_PACKET0)
-                const bool packet = MCPT_WF_PACKET0 && b == 0 && in_lds && MCPT_WF_IMPLICIT0 >= 2 &&
-                                    implicit0(kb, wf) && wf.group_shift == 6u;
-                if (packet)
+                if (packet && b == 0)
                     e = launch_extend_primary<4, kLdsBlock>(kb, wf, (int)nseg, lds_bytes_in_lds(img, 4) + 32, bs);
                 else if (in_lds)
                     e = launch_extend<true, 4, kLdsBlock>(kb, wf, (int)nseg, lds_bytes_in_lds(img, 4) + 32, bs);
