@@ -102,9 +102,14 @@ inline int DestroyGeometry() {       // CUTracer.cu:316-338, freeing what was al
 // hostcolor (width*height PWVector3f, row-major y*W+x) holds the running mean after
 // every launch (prevCount semantics, CUTracer.cu:215-217).  Camera of sceneID as
 // CUTracer.cu:347-374.  No OpenCV window / PNG side effects.
+// Summation order: by default the reference's -- each launch sums all of its
+// spp_per_kernel samples of a pixel in sample order, then divides
+// (CUTracer.cu:192-214; spp_chunk = 0).  A positive spp_chunk sums chunks of
+// that many samples first and the chunk sums in order (an explicit deviation:
+// the same image within fp32 rounding, not bit for bit).
 template <class Vec3T>
 int RenderScene(const int sceneID, Vec3T* hostcolor, int width = 800, int height = 600,
-                int num_kernels = 100, int spp_per_kernel = 100) {
+                int num_kernels = 100, int spp_per_kernel = 100, int spp_chunk = 0) {
     static_assert(sizeof(Vec3T) == 3 * sizeof(float), "hostcolor must be 3 packed floats per pixel");
     if (!detail::scene()) return MCPT_E_INVALID;
     mcpt_render_params p;
@@ -112,7 +117,7 @@ int RenderScene(const int sceneID, Vec3T* hostcolor, int width = 800, int height
     p.width = width;
     p.height = height;
     p.spp = static_cast<uint32_t>(spp_per_kernel);
-    p.spp_chunk = 32;
+    p.spp_chunk = static_cast<uint32_t>(spp_chunk > 0 ? spp_chunk : 0);
     p.eye[2] = (sceneID == 1) ? 17.0f : 23.0f;
     for (int k = 0; k < num_kernels; ++k) {
         p.spp_offset = static_cast<uint32_t>(k * spp_per_kernel);

@@ -125,6 +125,9 @@ struct mcpt_scene {
     std::vector<Timing> pending, free_timing;
     int last_variant = 0;
     uint64_t renders = 0;
+    // wavefront queue bytes set aside by mcpt_scene_reserve: later renders with a
+    // default batch never grow past them (no hipMalloc inside a stream capture)
+    size_t wf_reserved = 0;
     // multi-device scene (mcpt_init with n > 1): the primary (this object, on
     // devices[0]) owns one replica per further device -- the same image and
     // normals, its own workspace, a non-blocking stream and a completion event --
@@ -556,7 +559,17 @@ void fit_wavefront(const mcpt_scene& s, Plan& pl) {
     if (!budget) {
         size_t fr = 0, tot = 0;
         HIP_TRY(hipMemGetInfo(&fr, &tot));
-        budget = static_cast<uint64_t>((static_cast<double>(fr) + static_cast<double>(s.ws.wf_bytes)) * 0.9);
+        // what prepare_workspace will still allocate beside the queues (partial
+        // sums, stack spill areas) comes out of the same free memory
+        const mcpt::KernelParams& k = pl.kp;
+        const size_t lanes = static_cast<size_t>(mcpt::total_lanes_for(s.gpu.image_bytes, s.cus));
+        const size_t partial = size_t(k.nchunks) * k.npix_local * 16, spill = size_t(pl.wf_streams) * 32 * lanes * 16;
+        const double others = double(partial > s.ws.partial_bytes ? partial - s.ws.partial_bytes : 0) +
+                              double(spill > s.ws.spill_bytes ? spill - s.ws.spill_bytes : 0);
+        const double avail = (static_cast<double>(fr) + static_cast<double>(s.ws.wf_bytes)) * 0.9 - others;
+        budget = avail > 0 ? static_cast<uint64_t>(avail) : 0;
+        // a reserved scene keeps its reservation: a default batch is fitted into it
+        if (s.wf_reserved && !pl.wf_batch_explicit) budget = std::min<uint64_t>(budget, s.wf_reserved);
     }
     auto need = [&](uint64_t cap) { return uint64_t(wf_layout(s, pl, cap).need) * uint64_t(pl.wf_streams); };
     uint64_t cap = pl.wf_capacity;
@@ -566,7 +579,7 @@ void fit_wavefront(const mcpt_scene& s, Plan& pl) {
         char msg[256];
         std::snprintf(msg, sizeof msg,
                       "wavefront queues for batches of %llu paths need %.2f GB on %d stream(s); budget %.2f GB "
-                      "(wf_mem_limit or 90%% of free device memory): lower wf_batch / wf_streams",
+                      "(wf_mem_limit, the scene's reservation or 90%% of free device memory): lower wf_batch / wf_streams",
                       static_cast<unsigned long long>(cap), need(cap) / 1e9, pl.wf_streams, budget / 1e9);
         throw mcpt::Error{MCPT_E_NOMEM, msg};
     }
@@ -869,6 +882,8 @@ int mcpt_init(const int32_t* devices, int32_t n) {
         // multi-device gather's hipMemcpyPeerAsync is a direct xGMI DMA (without
         // it the runtime stages the copy through host memory); "already
         // enabled" is success, a pair without peer capability keeps the staged copy
+        // (the guard restores the caller's device if a HIP call throws mid-loop)
+        DeviceGuard guard;
         bool peer_ok = true;
         for (int i = 0; i < n; ++i)
             for (int j = 0; j < n; ++j) {
@@ -884,9 +899,9 @@ int mcpt_init(const int32_t* devices, int32_t n) {
                 if (e == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
                 else HIP_TRY(e);
             }
-        HIP_TRY(hipSetDevice(devices[0]));
         g_devices.assign(devices, devices + n);
         g_peer_ok = peer_ok;
+        guard.prev = devices[0];          // success: devices[0] becomes current
         return MCPT_OK;
     });
 }
@@ -1308,6 +1323,7 @@ int mcpt_scene_reserve(mcpt_scene* s, const mcpt_render_params* p) {
             if (pl.pipeline == MCPT_PIPELINE_WAVEFRONT) {
                 mcpt::WfParams wf[mcpt::kMaxWfStreams];
                 prepare_wavefront(sc, pl, sets, wf);
+                sc.wf_reserved = std::max(sc.wf_reserved, sc.ws.wf_bytes);
                 ensure_wf_streams(sc, sets);   // streams and events exist before any capture
             }
         };
@@ -1335,7 +1351,7 @@ int mcpt_scene_reserve(mcpt_scene* s, const mcpt_render_params* p) {
 
 int mcpt_plan_query(mcpt_scene* s, const mcpt_render_params* p, mcpt_plan_info* out) {
     return guarded([&]() -> int {
-        if (!s || !s->on_device || !out) return fail(MCPT_E_INVALID, "NULL argument or host-only scene");
+        if (!s || !s->on_device || !p || !out) return fail(MCPT_E_INVALID, "NULL argument or host-only scene");
         DeviceGuard guard;
         // a multi-device render: the plan of devices[0]'s shard (the largest)
         mcpt_render_params q = *p;

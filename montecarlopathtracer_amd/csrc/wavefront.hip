@@ -821,7 +821,8 @@ __global__ void __launch_bounds__(BLOCK) wf_shade_slots(const KernelParams kp, c
     // the material table in LDS when it fits beside the co-resident extend
     // (GEO_LDS): its fields are read in the branches of the shading chain,
     // each a dependent round trip that LDS serves in a fraction of L2's time
-    extern __shared__ GpuGeom lgeo[];
+    // (16-B aligned: it is filled through uint4 stores and read as whole records)
+    extern __shared__ __attribute__((aligned(16))) GpuGeom lgeo[];
     const WfCounters* cn = wf.cnt + (size_t)wf.bounce * wf.nseg + g;
     WfCounters* nx = wf.cnt + (size_t)(wf.bounce + 1) * wf.nseg + g;
     const uint32_t total = cn->queued;
@@ -1064,8 +1065,9 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams* wf_in, co
             // bounce 0 of CV mode (implicit queue 0: every origin is the eye): the
             // wave-coherent extend, one tree walk per 64-ray tile (MCPT_WF_PACKET0),
             // which also generates the primary rays (MCPT_WF_GEN0)
-            const bool packet = MCPT_WF_PACKET0 && in_lds && MCPT_WF_IMPLICIT0 >= 2 && implicit0(kb, wf) &&
-                                wf.group_shift == 6u;
+            // (the packet extend stores hit ids only: it needs MCPT_WF_HIT_ID's shade)
+            const bool packet = MCPT_WF_PACKET0 && MCPT_WF_HIT_ID && in_lds && MCPT_WF_IMPLICIT0 >= 2 &&
+                                implicit0(kb, wf) && wf.group_shift == 6u;
             if (!(packet && MCPT_WF_GEN0)) {
                 const uint32_t gen_grid = (n + kGenBlock - 1) / kGenBlock;
                 hipLaunchKernelGGL(wf_generate, dim3(gen_grid < 16u * (uint32_t)cus ? gen_grid : 16u * (uint32_t)cus),

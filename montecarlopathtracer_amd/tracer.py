@@ -390,12 +390,15 @@ class Tracer:
     def render_scene(self, scene_id: int, hostcolor: np.ndarray, num_kernels: int = NUM_KERNELS,
                      samples_per_kernel: int = NUM_SAMPLES_PER_KERNEL, callback=None, **kw) -> int:
         """RenderScene (CUTracer.cu:340-404): num_kernels launches of samples_per_kernel
-        samples; after launch k the buffer holds the running mean (prevCount = k)."""
+        samples; after launch k the buffer holds the running mean (prevCount = k).
+        Each launch sums its samples of a pixel in sample order, then divides
+        (CUTracer.cu:192-214): spp_chunk 0 unless the caller passes another."""
         if self.scene is None:
             raise McptError(-1, "CreateGeometry has not been called")
         H, W = hostcolor.shape[:2]
         stats = {}
         for each in range(num_kernels):
+            kw.setdefault("spp_chunk", 0)
             p = RenderParams.for_scene(scene_id, width=W, height=H, spp=samples_per_kernel,
                                        spp_offset=each * samples_per_kernel, prev_count=each, **kw)
             _, st = self.scene.render(p, hostcolor)

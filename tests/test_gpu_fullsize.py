@@ -11,8 +11,8 @@ statistical pin against the reference's own 1000-spp render.
   counters; and C5 (4096 spp) likewise, twice (determinism); its 2 and 8
   packed shards (one rank's work in bench.py's N-GPU runs) reassemble it.
 * every BASELINE config at its own sample count against the oracle: 128x128
-  crops of the whole C2 frame (light, glass sphere, miss corner), a 64x64 crop
-  of C4 (1024 spp) and of C5 (4096 spp), both pipelines, bit for bit, with the
+  crops of the whole C2 frame (light, glass sphere, miss corner), a 32x32 crop
+  of C4 (1024 spp), a 64x64 crop of C5 (4096 spp), both pipelines, bit for bit, with the
   megakernel's per-unit counters summed over the crop equal to the oracle's.
 * RenderScene's progressive loop (10 launches x 100 spp, prevCount running
   mean, CUTracer.cu:378-398) at 800x600 with the published-render variant

@@ -108,9 +108,12 @@ def test_device_render_deterministic(mcpt):
     assert np.array_equal(outs[0][..., :3], host)
 
 
-def test_pw_tracer_adapter_matches_abi(mcpt, tmp_path):
+def test_pw_tracer_adapter_matches_abi(mcpt, oracle_mod, tmp_path):
     """Reference-style call sequence through include/mcpt_pw_tracer.hpp renders what
-    the Python mirror renders (RenderScene: 3 launches x 4 spp, prevCount mean)."""
+    the Python mirror renders (RenderScene: 3 launches x 40 spp, prevCount mean),
+    in the reference's summation order -- each launch sums all 40 samples of a
+    pixel, then divides (CUTracer.cu:192-214, spp_chunk 0) -- and that is the
+    oracle's image at spp_chunk 0, bit for bit."""
     import os
     import subprocess
     import sys
@@ -118,14 +121,21 @@ def test_pw_tracer_adapter_matches_abi(mcpt, tmp_path):
     import build_dropin
     exe = build_dropin.build()
     out = str(tmp_path / "img.bin")
-    r = subprocess.run([exe, mcpt.scene_path("scene01"), out], capture_output=True, text=True)
+    spk = 40
+    r = subprocess.run([exe, mcpt.scene_path("scene01"), out, "", str(spk)], capture_output=True, text=True)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
     got = np.fromfile(out, np.float32).reshape(30, 40, 3)
     tr = mcpt.Tracer()
     tr.create_geometry(mcpt.ObjModel(mcpt.scene_path("scene01")))
     host = np.zeros((30, 40, 3), np.float32)
-    tr.render_scene(1, host, num_kernels=3, samples_per_kernel=4)
+    tr.render_scene(1, host, num_kernels=3, samples_per_kernel=spk)
     assert np.array_equal(got, host)
+    path = mcpt.scene_path("scene01")
+    ref = np.zeros((30, 40, 3), np.float32)
+    for k in range(3):
+        ref, _ = _oracle_render(oracle_mod, path, 40, 30, spk, 0, 7, mcpt.tracer.DEFAULT_SEED, 1, 10.0, 1,
+                                offset=k * spk, prev=ref, prev_count=k)
+    assert np.array_equal(got, ref), f"max abs diff {np.abs(got - ref).max()}"
 
 
 @pytest.mark.parametrize("streams", [1, 2, 3, 4])
