@@ -158,6 +158,8 @@ def wavefront_hbm(args, shard=(1, 0)) -> dict:
     w = pmc_pass(args, ["WRITE_SIZE"], "wf_write", reader=read_wf_kernels, shard=shard)
     v = pmc_pass(args, ["SQ_INSTS_VALU", "SQ_THREAD_CYCLES_VALU", "SQ_ACTIVE_INST_VALU", "SQ_WAVE_CYCLES",
                         "GRBM_GUI_ACTIVE"], "wf_valu", reader=read_wf_kernels, shard=shard)
+    ld = pmc_pass(args, ["SQ_INSTS_LDS", "SQ_LDS_IDX_ACTIVE", "SQ_LDS_BANK_CONFLICT", "GRBM_GUI_ACTIVE"], "wf_lds",
+                  reader=read_wf_kernels, shard=shard)
     res = {}
     for cls in f:
         if cls not in w or "FETCH_SIZE" not in f[cls] or "WRITE_SIZE" not in w[cls]:
@@ -170,7 +172,53 @@ def wavefront_hbm(args, shard=(1, 0)) -> dict:
                     "GBps": round((rd + wr) / max(ns, 1), 1), "frac": round((rd + wr) / max(ns, 1) / HBM_PEAK_GBS, 4)}
         if cls in v:
             res[cls]["valu_counters"] = {k: v[cls][k] for k in v[cls] if k.startswith(("SQ_", "GRBM_"))}
+        if cls in ld:
+            res[cls]["lds_counters"] = {k: ld[cls][k] for k in ld[cls] if k.startswith(("SQ_", "GRBM_"))}
+            res[cls]["lds_counters"]["ns"] = ld[cls]["ns"]
     return res
+
+
+LDS_PEAK_GBS = 150000.0   # MI355X_MICROARCH.md LDS: ~150 TB/s aggregate ds_read_b64/b128, every CU streaming
+
+
+def lds_block(pmc: dict, cus: int, per_frame: dict) -> dict:
+    """The LDS side of the traversal (scene image and stack in LDS): the LDS
+    array's busy fraction measured by SQ_LDS_IDX_ACTIVE (all LDS-array cycles,
+    summed over CUs) / (CUs x cycles), cycles = GRBM_GUI_ACTIVE / 8 XCDs; and
+    the bytes the walk reads from LDS by its own records (16-B sibling pair per
+    inner step, 4-B leaf ref, 48-B triangle record per test) over the extend's
+    time against the guide's aggregate LDS read rate."""
+    if not (pmc.get("SQ_LDS_IDX_ACTIVE") and pmc.get("GRBM_GUI_ACTIVE") and pmc.get("ns")):
+        return {}
+    cycles = pmc["GRBM_GUI_ACTIVE"] / 8.0
+    busy = pmc["SQ_LDS_IDX_ACTIVE"] / (cus * cycles)
+    lds_bytes = (16 * per_frame["inner_visits"] + 4 * per_frame["leaf_refs"] + 48 * per_frame["tri_tests"])
+    gbs = lds_bytes / pmc["ns"]
+    out = {"array_busy_frac": round(busy, 4), "achieved": round(gbs, 1), "peak": LDS_PEAK_GBS, "unit": "GB/s",
+           "frac": round(gbs / LDS_PEAK_GBS, 4), "traffic": round(lds_bytes / 1e9, 3),
+           "traffic_unit": "GB per frame read from LDS by the walk's records (16 x inner + 4 x leaf refs + 48 x "
+                           "triangle tests)",
+           "lds_instr_G": round(pmc.get("SQ_INSTS_LDS", 0.0) / 1e9, 3),
+           "formula": "array_busy = SQ_LDS_IDX_ACTIVE / (CUs * GRBM_GUI_ACTIVE/8); achieved = traffic / extend ns"}
+    if pmc.get("SQ_INSTS_LDS"):
+        out["conflict_cycles_per_lds_instr"] = round(pmc.get("SQ_LDS_BANK_CONFLICT", 0.0) / pmc["SQ_INSTS_LDS"], 3)
+    return out
+
+
+def binding_of(roof: dict) -> dict:
+    """Which roof the dominant kernel is nearest: the largest of its HBM
+    fraction, LDS-array busy fraction and VALU issue fraction."""
+    cands = {}
+    if roof.get("frac") is not None:
+        cands["hbm"] = roof["frac"]
+    if roof.get("lds", {}).get("array_busy_frac") is not None:
+        cands["lds_array"] = roof["lds"]["array_busy_frac"]
+    if roof.get("valu", {}).get("issue_frac") is not None:
+        cands["valu_issue"] = roof["valu"]["issue_frac"]
+    if not cands:
+        return {}
+    name = max(cands, key=cands.get)
+    return {"binding_frac": cands[name], "binding": name, "fracs": cands}
 
 
 def valu_block(pmc: dict, cus: int, kern_ms: float, rays: float) -> dict:
@@ -317,6 +365,8 @@ def main():
                     help="set a scheduling field of the render params (wf_refill, ready_thresh, wf_group_shift, "
                          "tail_units_per_lane, wf_mem_limit, ...; never changes the image) -- for sweeps")
     ap.add_argument("--keep-pmc", default="", help="copy the raw rocprofv3 PMC csv files into this directory")
+    ap.add_argument("--dump-image", default="", help="rank 0 saves the last timed step's (gathered) image here "
+                                                     "as a (H, W, 4) float32 .npy (tests)")
     ap.add_argument("--pmc-shard", default="1,0", help=argparse.SUPPRESS)   # PMC child: shard count,index
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = this process's CPU share (<= 16)")
@@ -425,6 +475,10 @@ def main():
 
     # the other pipeline on the same frame, for comparison (N = 1; same image, bit for bit)
     alt = None
+    if args.dump_image and rank == 0:   # before the comparison renders reuse fb
+        import numpy as np
+        img = gatherer.image if gatherer is not None else fb
+        np.save(args.dump_image, img.view(args.height, args.width, 4).cpu().numpy())
     if n_gpus == 1 and not args.no_alt:
         other = "megakernel" if args.pipeline == "wavefront" else "wavefront"
         pa = dataclasses.replace(p, pipeline=other)
@@ -496,8 +550,16 @@ def main():
                 if vb:
                     vb["kernel"] = "wf_extend (the traversal: the dominant kernel), run alone"
                     roof["valu"] = vb
+                # rank 0's shard: its share of the frame's counts (interleaved tiles, ~1/N)
+                lb = lds_block(ext.pop("lds_counters", {}), cus,
+                               {k: per_launch[k] / n_gpus for k in ("inner_visits", "leaf_refs", "tri_tests")})
+                if lb:
+                    lb["kernel"] = "wf_extend, run alone"
+                    roof["lds"] = lb
+                roof.update(binding_of(roof))
             for k in kh.values():
                 k.pop("valu_counters", None)
+                k.pop("lds_counters", None)
             if kh:
                 tot_b = sum((k["hbm_read_GB"] + k["hbm_write_GB"]) for k in kh.values())
                 pg = tot_b / (kern_ms * 1e-3) if kern_ms > 0 else 0.0

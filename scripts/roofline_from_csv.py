@@ -2,8 +2,11 @@
 """Recompute a bench line's wf_extend roofline from the raw rocprofv3 PMC csv it
 kept (bench.py --keep-pmc DIR; committed under profiles/rNN/pmc_wf):
 achieved = (2 x FETCH_SIZE + WRITE_SIZE) KiB of the extend dispatches / their
-summed duration in the FETCH_SIZE pass, frac = achieved / 8000 GB/s.
-usage: roofline_from_csv.py profiles/r03/pmc_wf [profiles/r03/bench.jsonl]"""
+summed duration in the FETCH_SIZE pass, frac = achieved / 8000 GB/s; with the
+bench line (its per-ray counts, rays per frame and the CU count it ran on) also
+roofline.lds from the wf_lds pass and roofline.binding_frac (max of the HBM,
+LDS-array and VALU-issue fractions; the VALU figure from the wf_valu pass).
+usage: roofline_from_csv.py profiles/r04/pmc_wf [profiles/r04/bench.jsonl] [CUs=256]"""
 import importlib.util
 import json
 import os
@@ -12,7 +15,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def main(d, line=None):
+def main(d, line=None, cus=256):
     spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
     b = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(b)
@@ -23,8 +26,26 @@ def main(d, line=None):
     out = {"extend_read_GB": round(rd / 1e9, 3), "extend_write_GB": round(wr / 1e9, 3), "ms": round(f["ns"] / 1e6, 3),
            "launches": f["dispatches"], "achieved_GBps": round(gbs, 2), "frac": round(gbs / b.HBM_PEAK_GBS, 5)}
     if line:
-        r = [json.loads(x) for x in open(line) if x.startswith("{")][-1]["roofline"]
+        ln = [json.loads(x) for x in open(line) if x.startswith("{")][-1]
+        r = ln["roofline"]
         out["bench_line"] = {"achieved": r["achieved"], "frac": r["frac"], "traffic": r["traffic"]}
+        cus = int(cus)
+        roof = {"frac": out["frac"]}
+        vd = os.path.join(d, "wf_valu")
+        if os.path.isdir(vd):
+            v = b.read_wf_kernels(vd)["extend"]
+            roof["valu"] = b.valu_block(v, cus, v["ns"] / 1e6, ln["rays_per_step"] / ln["n_gpus"])
+        ldd = os.path.join(d, "wf_lds")
+        if os.path.isdir(ldd):
+            lc = b.read_wf_kernels(ldd)["extend"]
+            pr = r["algorithmic"]["per_ray"]
+            rays = ln["rays_per_step"] / ln["n_gpus"]
+            roof["lds"] = b.lds_block(lc, cus, {k: pr[k] * rays for k in ("inner_visits", "leaf_refs", "tri_tests")})
+            out["lds"] = roof["lds"]
+            out["bench_line"]["lds"] = r.get("lds")
+        out.update(b.binding_of(roof))
+        out["bench_line"]["binding_frac"] = r.get("binding_frac")
+        out["bench_line"]["binding"] = r.get("binding")
     print(json.dumps(out))
 
 

@@ -67,3 +67,22 @@ def test_path_kernel_reader_picks_the_lean_kernel(tmp_path):
     ])
     # per-launch average over the lean kernel's dispatches: (10 + 20) / 2
     assert read_counters(str(tmp_path / "q")) == {"WRITE_SIZE": 15.0}
+
+
+def test_lds_block_and_binding_roof():
+    b = _bench()
+    cus = 256
+    # 1e6 kernel cycles (GRBM summed over 8 XCDs), LDS array busy 0.4 of every CU's cycles
+    pmc = {"SQ_LDS_IDX_ACTIVE": 0.4 * cus * 1e6, "GRBM_GUI_ACTIVE": 8e6, "SQ_INSTS_LDS": 1e6,
+           "SQ_LDS_BANK_CONFLICT": 2.5e6, "ns": 1e6}
+    per = {"inner_visits": 1e6, "leaf_refs": 2e5, "tri_tests": 3e5}
+    lb = b.lds_block(pmc, cus, per)
+    assert lb["array_busy_frac"] == 0.4
+    assert lb["traffic"] == round((16e6 + 4 * 2e5 + 48 * 3e5) / 1e9, 3)
+    assert lb["achieved"] == round((16e6 + 8e5 + 1.44e7) / 1e6, 1)      # bytes / ns = GB/s
+    assert lb["conflict_cycles_per_lds_instr"] == 2.5
+    bd = b.binding_of({"frac": 0.08, "lds": lb, "valu": {"issue_frac": 0.55}})
+    assert bd["binding"] == "valu_issue" and bd["binding_frac"] == 0.55
+    assert set(bd["fracs"]) == {"hbm", "lds_array", "valu_issue"}
+    assert b.binding_of({"frac": 0.9, "lds": lb})["binding"] == "hbm"
+    assert b.lds_block({}, cus, per) == {}

@@ -8,8 +8,9 @@ statistical pin against the reference's own 1000-spp render.
   single-GPU image bit for bit; a second render is bit-identical (determinism);
   the image is finite and the light is the brightest region.
 * the same frame through the wavefront pipeline: bit-identical image, equal
-  counters; and C5 (4096 spp) likewise, twice (determinism); its 2 and 8
-  packed shards (one rank's work in bench.py's N-GPU runs) reassemble it.
+  counters; and C5 (4096 spp) likewise, twice (determinism); the C2 frame's
+  2 and 8 packed shards and C5's 8 (one rank's work in bench.py's N-GPU runs)
+  reassemble them.
 * every BASELINE config at its own sample count against the oracle: 128x128
   crops of the whole C2 frame (light, glass sphere, miss corner), a 32x32 crop
   of C4 (1024 spp), a 64x64 crop of C5 (4096 spp), both pipelines, bit for bit, with the
@@ -245,6 +246,25 @@ def test_c5_wavefront_equals_megakernel_and_is_deterministic(mcpt, scene01):
         assert torch.equal(img[:, :3], ref[:, :3]), name
         for k in ("rays", "paths", "inner_visits", "leaf_visits", "tri_tests", "shades"):
             assert st[k] == rs[k], (name, k, st[k], rs[k])
+    # C5's split (BASELINE configs[4]: 4096 spp on 8 GPUs): the 8 packed
+    # wavefront shards one rank each renders (lean, as bench.py times them)
+    # reassemble the whole frame bit for bit, with the frame's rays
+    N = 8
+    got = torch.full((H * W, 4), -1.0, dtype=torch.float32, device="cuda")
+    rays = 0
+    for r in range(N):
+        ps = mcpt.RenderParams(width=W, height=H, spp=4096, spp_chunk=32, shard_count=N, shard_index=r,
+                               packed=True, tile=8, pipeline="wavefront", lean=True)
+        part = torch.zeros((ps.output_pixels(), 4), dtype=torch.float32, device="cuda")
+        scene01.render_device(ps, part.data_ptr(), stream)
+        torch.cuda.synchronize()
+        rays += scene01.stats()["rays"]
+        xy = torch.from_numpy(ps.shard_pixels().astype(np.int64)).cuda()
+        ok = xy[:, 0] >= 0
+        got[(xy[:, 1] * W + xy[:, 0])[ok]] = part[ok]
+    torch.cuda.synchronize()
+    assert torch.equal(got[:, :3], ref[:, :3])
+    assert rays == rs["rays"]
 
 
 def test_progressive_render_matches_reference_image(mcpt):
