@@ -359,6 +359,9 @@ def main():
     ap.add_argument("--single-process", action="store_true",
                     help="one process drives all --gpus devices through mcpt_init(devices) (the C ABI's "
                          "multi-device render: replicas, peer-copy gather) instead of one rank per GPU")
+    ap.add_argument("--gather", choices=["peer", "rccl"], default="peer",
+                    help="--single-process: how the shards reach device 0 (mcpt_render_params::gather): peer "
+                         "copies or one ncclGather over a communicator of the device list")
     ap.add_argument("--devices", default="", help="--single-process device list (default 0..gpus-1); a repeated "
                                                   "ordinal rehearses the multi-device path on one GPU, e.g. 0,0")
     ap.add_argument("--set", action="append", default=[], metavar="FIELD=VALUE",
@@ -429,7 +432,7 @@ def main():
     p = M.RenderParams.for_scene(scene_id, width=args.width, height=args.height, spp=args.spp,
                                  spp_chunk=args.spp_chunk, tile=8, shard_count=world, shard_index=rank,
                                  packed=world > 1, pipeline=args.pipeline, wf_batch=args.wf_batch,
-                                 wf_streams=args.wf_streams, lean=lean, **_tuning(args))
+                                 wf_streams=args.wf_streams, lean=lean, gather=args.gather, **_tuning(args))
     p_count = dataclasses.replace(p, lean=False)
     n_out = p.output_pixels()
     fb = torch.zeros((n_out, 4), dtype=torch.float32, device=dev)
@@ -615,7 +618,8 @@ def main():
         sched["workspace_GB"] = round(plan["workspace_bytes"] / 1e9, 2)
         if n_gpus > 1:
             par = (f"pixel-tiles x{n_gpus} + " + (f"{'rccl' if backend == 'nccl' else backend} gather" if world > 1
-                                                  else f"peer-copy gather (one process, mcpt_init({devices}))"))
+                                                  else f"{'peer-copy' if args.gather == 'peer' else 'rccl'} gather "
+                                                       f"(one process, mcpt_init({devices}))"))
         else:
             par = "pixel-tiles x1"
         line = {

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define MCPT_ABI_VERSION 6
+#define MCPT_ABI_VERSION 7
 
 enum {
     MCPT_OK = 0,
@@ -125,8 +125,18 @@ typedef struct {
     int32_t force_peer_copy;    /* multi-device renders: gather every shard with hipMemcpyPeerAsync,
                                    also between replicas on one device (exercises the cross-device
                                    path on a one-GPU box); 0: peer copies between devices only */
-    int32_t reserved_;          /* 0 */
+    int32_t gather;             /* multi-device renders (mcpt_init with a device list): how the shards
+                                   reach devices[0].  MCPT_GATHER_PEER (0): one hipMemcpyPeerAsync
+                                   per device (xGMI DMA).  MCPT_GATHER_RCCL: one ncclGather over a
+                                   communicator of the device list (ncclCommInitAll, created on
+                                   first use; librccl is loaded then) -- also for a one-device
+                                   list, where it is a one-rank gather.  Same image either way */
 } mcpt_render_params;
+
+enum {
+    MCPT_GATHER_PEER = 0,
+    MCPT_GATHER_RCCL = 1
+};
 
 enum {
     /* CVMCTracer/CUDA/CUTracer.cu:98-218: 7 scatters + terminal query, ILLUM,
@@ -203,8 +213,9 @@ const char* mcpt_last_error(void);
  * n_devices interleaved-tile shards (tile t -> device t % n), rendered
  * concurrently, peer-copied to devices[0] (xGMI DMA) and unpermuted there --
  * the single-device image bit for bit; stats sum the devices.  A device may
- * be listed twice (two replicas on one GPU).  n_devices == 0 keeps the
- * current device and a single-device scene. */
+ * be listed twice (two replicas on one GPU; RCCL refuses such a list for its
+ * gather, mcpt_render_params::gather).  n_devices == 0 keeps the current
+ * device and a single-device scene. */
 int mcpt_init(const int32_t* devices, int32_t n_devices);
 int mcpt_device_count(int32_t* out);
 /* fill defaults = the CVMCTracer constants for scene 1 (CUTracer.cu:347-360) */

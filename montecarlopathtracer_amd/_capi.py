@@ -21,11 +21,13 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MCPT_LIB_PATH") or os.path.join(_HERE, "lib", "libmcpt.so")
 
 MCPT_OK = 0
-ABI_VERSION = 6
+ABI_VERSION = 7
 MODE_CVMCTRACER = 0
 MODE_QUINENGINE = 1
 PIPELINE_MEGAKERNEL = 0
 PIPELINE_WAVEFRONT = 1
+GATHER_PEER = 0
+GATHER_RCCL = 1
 ERRORS = {-1: "INVALID", -2: "IO", -3: "PARSE", -4: "DEVICE", -5: "NOMEM", -6: "UNSUPPORTED"}
 
 
@@ -58,7 +60,7 @@ class RenderParamsC(C.Structure):
         ("wf_sort", C.c_int32),
         ("wf_streams", C.c_int32), ("wf_refill", C.c_int32), ("wf_group_shift", C.c_int32),
         ("ready_thresh", C.c_int32), ("tail_units_per_lane", C.c_int32), ("tail_units", C.c_int32),
-        ("wf_mem_limit", C.c_uint64), ("force_peer_copy", C.c_int32), ("reserved_", C.c_int32),
+        ("wf_mem_limit", C.c_uint64), ("force_peer_copy", C.c_int32), ("gather", C.c_int32),
     ]
 
 

@@ -5,7 +5,9 @@
 // (DestroyGeometry, here freeing exactly what was allocated) and the render
 // entry (RenderScene).  Unlike the reference, no module globals hold the scene:
 // every call takes the opaque handle it works on.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>   // types and prototypes only: librccl is loaded on first use (rccl())
 
 #include <algorithm>
 #include <cfloat>
@@ -109,6 +111,49 @@ struct DeviceGuard {
     }
 };
 
+// RCCL, resolved from librccl at the first render that asks for its gather
+// (mcpt_render_params::gather): libmcpt itself does not depend on it, so it
+// loads where RCCL is absent and a one-process renderer that never asks pays
+// nothing for it.
+struct Rccl {
+    decltype(&ncclCommInitAll) comm_init_all = nullptr;
+    decltype(&ncclCommDestroy) comm_destroy = nullptr;
+    decltype(&ncclGather) gather = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
+    decltype(&ncclGetErrorString) error_string = nullptr;
+    std::string load_error;
+};
+const Rccl& rccl() {
+    static const Rccl r = [] {
+        Rccl x;
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) {
+            const char* e = dlerror();
+            x.load_error = std::string("cannot load librccl: ") + (e ? e : "?");
+            return x;
+        }
+        x.comm_init_all = reinterpret_cast<decltype(&ncclCommInitAll)>(dlsym(h, "ncclCommInitAll"));
+        x.comm_destroy = reinterpret_cast<decltype(&ncclCommDestroy)>(dlsym(h, "ncclCommDestroy"));
+        x.gather = reinterpret_cast<decltype(&ncclGather)>(dlsym(h, "ncclGather"));
+        x.group_start = reinterpret_cast<decltype(&ncclGroupStart)>(dlsym(h, "ncclGroupStart"));
+        x.group_end = reinterpret_cast<decltype(&ncclGroupEnd)>(dlsym(h, "ncclGroupEnd"));
+        x.error_string = reinterpret_cast<decltype(&ncclGetErrorString)>(dlsym(h, "ncclGetErrorString"));
+        if (!x.comm_init_all || !x.comm_destroy || !x.gather || !x.group_start || !x.group_end || !x.error_string)
+            x.load_error = "librccl lacks ncclCommInitAll / ncclGather / ncclGroupStart / ncclGroupEnd";
+        return x;
+    }();
+    return r;
+}
+
+#define NCCL_TRY(expr)                                                                                  \
+    do {                                                                                                \
+        ncclResult_t r_ = (expr);                                                                       \
+        if (r_ != ncclSuccess)                                                                          \
+            throw mcpt::Error{MCPT_E_DEVICE, std::string(#expr) + ": " + rccl().error_string(r_)};   \
+    } while (0)
+
 }  // namespace
 
 struct mcpt_scene {
@@ -143,6 +188,11 @@ struct mcpt_scene {
     hipStream_t wf_stream[mcpt::kMaxWfStreams] = {};   // [0] unused (the caller's)
     hipEvent_t wf_fork = nullptr, wf_join[mcpt::kMaxWfStreams] = {};
     bool peer_access = true;            // multi-device: peer access enabled between every device pair
+    // multi-device, gather = RCCL: one communicator per device of the list
+    // (ncclCommInitAll, rank r = device r of the list) and rank 0's send buffer
+    std::vector<ncclComm_t> comms;
+    void* gather_send = nullptr;
+    size_t gather_send_bytes = 0;
 
     ~mcpt_scene() {
         if (!on_device) return;
@@ -150,7 +200,15 @@ struct mcpt_scene {
         (void)hipGetDevice(&prev);
         (void)hipSetDevice(device);
         (void)hipDeviceSynchronize();
-        for (void* p : {d_image, d_normals, ws.partial, ws.small, ws.spill, ws.fb, ws.wf, ws.tail, gather})
+        if (!comms.empty()) {               // no collective in flight on any device, then the comms
+            for (auto& R : replicas) {
+                (void)hipSetDevice(R->device);
+                (void)hipDeviceSynchronize();
+            }
+            for (ncclComm_t c : comms) (void)rccl().comm_destroy(c);
+            (void)hipSetDevice(device);
+        }
+        for (void* p : {d_image, d_normals, ws.partial, ws.small, ws.spill, ws.fb, ws.wf, ws.tail, gather, gather_send})
             if (p) (void)hipFree(p);
         for (auto& t : pending) for (auto ev : t.e) (void)hipEventDestroy(ev);
         for (auto& t : free_timing) for (auto ev : t.e) (void)hipEventDestroy(ev);
@@ -183,7 +241,33 @@ struct DeviceOrder {
     std::vector<uint32_t> leaf_order;   // host leaf nodes in device order
     std::vector<uint32_t> tri_order;    // device triangle slot -> kd id
     std::vector<uint32_t> tri_new;      // kd id -> device triangle slot
+    std::vector<uint8_t> group_root;    // device_order_groups: node is a group root (empty: no groups)
 };
+
+// leaves in device node order, triangles by first appearance (both layouts)
+void order_leaves(const mcpt::HostScene& hs, DeviceOrder& d) {
+    const uint32_t nn = static_cast<uint32_t>(hs.nodes.size());
+    std::vector<uint32_t> by_dev(d.n_slots, 0xFFFFFFFFu);
+    for (uint32_t i = 0; i < nn; ++i) by_dev[d.node_new[i]] = i;
+    d.tri_new.assign(hs.kd_tris.size(), 0xFFFFFFFFu);
+    for (uint32_t dv = 0; dv < d.n_slots; ++dv) {
+        const uint32_t i = by_dev[dv];
+        if (i == 0xFFFFFFFFu || hs.nodes[i].axis) continue;
+        d.leaf_order.push_back(i);
+        for (uint32_t r = 0; r < hs.nodes[i].leaf_count; ++r) {
+            const uint32_t k = hs.leaf_ids[hs.nodes[i].leaf_begin + r];
+            if (d.tri_new[k] == 0xFFFFFFFFu) {
+                d.tri_new[k] = static_cast<uint32_t>(d.tri_order.size());
+                d.tri_order.push_back(k);
+            }
+        }
+    }
+    for (uint32_t k = 0; k < d.tri_new.size(); ++k)
+        if (d.tri_new[k] == 0xFFFFFFFFu) {
+            d.tri_new[k] = static_cast<uint32_t>(d.tri_order.size());
+            d.tri_order.push_back(k);
+        }
+}
 
 DeviceOrder device_order(const mcpt::HostScene& hs) {
     const uint32_t nn = static_cast<uint32_t>(hs.nodes.size());
@@ -215,27 +299,55 @@ DeviceOrder device_order(const mcpt::HostScene& hs) {
         }
     }
     d.n_slots = 2 * pairs + 1;
-    // leaves in device order, triangles by first appearance
-    std::vector<uint32_t> by_dev(d.n_slots, 0xFFFFFFFFu);
-    for (uint32_t i = 0; i < nn; ++i) by_dev[d.node_new[i]] = i;
-    d.tri_new.assign(hs.kd_tris.size(), 0xFFFFFFFFu);
-    for (uint32_t dv = 0; dv < d.n_slots; ++dv) {
-        const uint32_t i = by_dev[dv];
-        if (i == 0xFFFFFFFFu || hs.nodes[i].axis) continue;
-        d.leaf_order.push_back(i);
-        for (uint32_t r = 0; r < hs.nodes[i].leaf_count; ++r) {
-            const uint32_t k = hs.leaf_ids[hs.nodes[i].leaf_begin + r];
-            if (d.tri_new[k] == 0xFFFFFFFFu) {
-                d.tri_new[k] = static_cast<uint32_t>(d.tri_order.size());
-                d.tri_order.push_back(k);
-            }
-        }
+    order_leaves(hs, d);
+    return d;
+}
+
+// Two-level node groups (8-B node images, MCPT_KD_GROUPS; trace_device.hpp
+// descend_steps): every inner node at even depth is a group root; its group
+// is its sibling pair followed by the pairs of its inner children (left
+// child's first), so the walk reads both levels below a root with one 48-B
+// read.  Groups are emitted breadth-first (the top of the tree first).  The
+// pair count -- hence the image size -- is the cluster order's.
+DeviceOrder device_order_groups(const mcpt::HostScene& hs) {
+    const uint32_t nn = static_cast<uint32_t>(hs.nodes.size());
+    DeviceOrder d;
+    d.node_new.assign(nn, 0xFFFFFFFFu);
+    d.group_root.assign(nn, 0);
+    d.node_new[0] = 0;
+    uint32_t pairs = 0;
+    auto place = [&](uint32_t L) {       // the pair (L, L+1) -> the next pair slot
+        d.node_new[L] = 2 * pairs + 1;
+        d.node_new[L + 1] = 2 * pairs + 2;
+        ++pairs;
+    };
+    std::vector<uint32_t> queue;
+    if (nn && hs.nodes[0].axis) queue.push_back(0);
+    for (size_t qi = 0; qi < queue.size(); ++qi) {
+        const uint32_t n = queue[qi];
+        d.group_root[n] = 1;
+        const uint32_t L = hs.nodes[n].left;
+        place(L);
+        for (uint32_t c = L; c <= L + 1; ++c)
+            if (hs.nodes[c].axis) place(hs.nodes[c].left);
+        for (uint32_t c = L; c <= L + 1; ++c)
+            if (hs.nodes[c].axis)
+                for (uint32_t g = hs.nodes[c].left; g <= hs.nodes[c].left + 1; ++g)
+                    if (hs.nodes[g].axis) queue.push_back(g);
     }
-    for (uint32_t k = 0; k < d.tri_new.size(); ++k)
-        if (d.tri_new[k] == 0xFFFFFFFFu) {
-            d.tri_new[k] = static_cast<uint32_t>(d.tri_order.size());
-            d.tri_order.push_back(k);
-        }
+    d.n_slots = 2 * pairs + 1;
+    // the walk's invariant (descend_steps): a root's inner child has its pair
+    // 1 or 2 pairs after the root's own, the left child's first
+    for (uint32_t n : queue) {
+        const uint32_t L = hs.nodes[n].left, base = d.node_new[L];
+        uint32_t at = base + 2;
+        for (uint32_t c = L; c <= L + 1; ++c)
+            if (hs.nodes[c].axis) {
+                if (d.node_new[hs.nodes[c].left] != at) throw mcpt::Error{MCPT_E_INVALID, "node group layout"};
+                at += 2;
+            }
+    }
+    order_leaves(hs, d);
     return d;
 }
 
@@ -276,8 +388,12 @@ void build_image(mcpt_scene& s, bool force_global) {
         boxes = true;
         total = image_size(ord, off_nodes, off_leafs, off_geoms);
     }
+    // 8-B node images: the two-level group order (same size)
+    if (!boxes && MCPT_KD_GROUPS) ord = device_order_groups(hs);
     const size_t off_tris = 0;
     if (total > 0xFFFFFFF0u) throw mcpt::Error{MCPT_E_UNSUPPORTED, "scene image exceeds 4 GiB"};
+    if (!ord.group_root.empty() && ord.n_slots >= (1u << 29))
+        throw mcpt::Error{MCPT_E_UNSUPPORTED, "KD tree too large for grouped node words"};
     if (ord.n_slots >= (1u << 30) || nl >= (1u << 30)) throw mcpt::Error{MCPT_E_UNSUPPORTED, "KD tree too large"};
     s.image.assign(total, 0);
     s.tri_order = ord.tri_order;
@@ -312,6 +428,7 @@ void build_image(mcpt_scene& s, bool force_global) {
         uint32_t w[2];
         if (n.axis) {
             w[0] = ((n.axis - 1u) << 30) | ord.node_new[n.left];
+            if (!ord.group_root.empty() && ord.group_root[i]) w[0] |= 1u << 29;   // trace_device.hpp kGroupBit
             std::memcpy(&w[1], &n.split, 4);
         } else {
             w[0] = (3u << 30) | leaf_begin_new[i];
@@ -674,7 +791,9 @@ void set_device(const mcpt_scene& s) {
 void render_multi(mcpt_scene& s, const mcpt_render_params* p, float* d_fb, hipStream_t st);
 
 bool multi_device(const mcpt_scene& s, const mcpt_render_params* p, const uint32_t* d_unit_counters) {
-    return !s.replicas.empty() && p && p->shard_count <= 1 && !p->packed && !d_unit_counters;
+    // (an RCCL gather also runs for a one-device list: a one-rank communicator)
+    return (!s.replicas.empty() || (p && p->gather == MCPT_GATHER_RCCL)) && p && p->shard_count <= 1 && !p->packed &&
+           !d_unit_counters;
 }
 
 void render_async(mcpt_scene& s, const mcpt_render_params* p, float* d_fb, hipStream_t st,
@@ -777,16 +896,44 @@ void read_stats(mcpt_scene& s, mcpt_render_stats* out) {
 // RNG is keyed per (pixel, sample), so the image is the single-device one bit
 // for bit.  Cross-device order: every shard waits for `start` (recorded on the
 // caller's stream), the caller's stream waits for every shard's `done`.
+// RCCL gather: one communicator per device of the list (ncclCommInitAll,
+// rank r = the list's device r), made once per scene
+void ensure_comms(mcpt_scene& s) {
+    if (!s.comms.empty()) return;
+    const Rccl& R = rccl();
+    if (!R.load_error.empty()) throw mcpt::Error{MCPT_E_UNSUPPORTED, R.load_error};
+    std::vector<int> devs{s.device};
+    for (auto& rep : s.replicas) devs.push_back(rep->device);
+    std::vector<ncclComm_t> comms(devs.size(), nullptr);
+    NCCL_TRY(R.comm_init_all(comms.data(), static_cast<int>(devs.size()), devs.data()));
+    s.comms = comms;
+}
+
+// packed pixels per shard slot of an n-way multi-device render (>= every shard's count)
+uint64_t multi_slot(const Plan& full, const mcpt_render_params* p, int n) {
+    const int T = full.kp.tile;
+    const uint64_t ntiles = uint64_t(full.kp.tiles_x) * ((uint64_t(p->height) + T - 1) / T);
+    return (ntiles + n - 1) / n * uint64_t(T) * uint64_t(T);
+}
+
 void render_multi(mcpt_scene& s, const mcpt_render_params* p, float* d_fb, hipStream_t st) {
     DeviceGuard guard;   // an error on a replica's device must not leave that device current
     set_device(s);
     const Plan full = make_plan(s, p);                  // validates p; row-major output
+    if (p->gather != MCPT_GATHER_PEER && p->gather != MCPT_GATHER_RCCL)
+        throw mcpt::Error{MCPT_E_INVALID, "unknown gather"};
+    const bool use_rccl = p->gather == MCPT_GATHER_RCCL;
     const int n = 1 + static_cast<int>(s.replicas.size());
     const int T = full.kp.tile;
-    const uint64_t ntiles = uint64_t(full.kp.tiles_x) * ((uint64_t(p->height) + T - 1) / T);
-    const uint64_t slot = (ntiles + n - 1) / n * uint64_t(T) * uint64_t(T);
+    const uint64_t slot = multi_slot(full, p, n);
     if (slot * n >= (uint64_t(1) << 32)) throw mcpt::Error{MCPT_E_UNSUPPORTED, "image too large"};
     ensure_buf(s.gather, s.gather_bytes, size_t(n) * slot * 16);
+    if (use_rccl) {
+        ensure_comms(s);
+        // every rank sends `slot` pixels (ncclGather's equal counts; the shards'
+        // own counts differ by at most one tile): rank 0 from gather_send
+        ensure_buf(s.gather_send, s.gather_send_bytes, size_t(slot) * 16);
+    }
     if (!s.start) HIP_TRY(hipEventCreateWithFlags(&s.start, hipEventDisableTiming));
     HIP_TRY(hipEventRecord(s.start, st));
     auto shard = [&](int r) {
@@ -801,9 +948,10 @@ void render_multi(mcpt_scene& s, const mcpt_render_params* p, float* d_fb, hipSt
         set_device(R);
         const mcpt_render_params pr = shard(r);
         const size_t bytes = size_t(mcpt_shard_pixel_count(&pr)) * 16;
-        ensure_buf(R.ws.fb, R.ws.fb_bytes, bytes);
+        ensure_buf(R.ws.fb, R.ws.fb_bytes, use_rccl ? size_t(slot) * 16 : bytes);
         HIP_TRY(hipStreamWaitEvent(R.stream, s.start, 0));
         render_async(R, &pr, static_cast<float*>(R.ws.fb), R.stream, nullptr, true);
+        if (use_rccl) continue;                        // gathered below, all ranks in one group
         char* dst = static_cast<char*>(s.gather) + size_t(r) * slot * 16;
         if (R.device == s.device && !p->force_peer_copy)
             HIP_TRY(hipMemcpyAsync(dst, R.ws.fb, bytes, hipMemcpyDeviceToDevice, R.stream));
@@ -813,7 +961,31 @@ void render_multi(mcpt_scene& s, const mcpt_render_params* p, float* d_fb, hipSt
     }
     set_device(s);
     const mcpt_render_params p0 = shard(0);
-    render_async(s, &p0, static_cast<float*>(s.gather), st, nullptr, true);
+    render_async(s, &p0, static_cast<float*>(use_rccl ? s.gather_send : s.gather), st, nullptr, true);
+    if (use_rccl) {
+        // ncclGather of every rank's `slot` packed pixels into devices[0]'s
+        // gather buffer (rank r at r * slot), each on the stream its shard was
+        // rendered on; one group, as one process drives every rank
+        const Rccl& R = rccl();
+        const size_t count = size_t(slot) * 4;
+        NCCL_TRY(R.group_start());
+        try {
+            for (int r = 0; r < n; ++r) {
+                const void* send = r ? s.replicas[size_t(r - 1)]->ws.fb : s.gather_send;
+                hipStream_t rs = r ? s.replicas[size_t(r - 1)]->stream : st;
+                NCCL_TRY(R.gather(send, r ? nullptr : s.gather, count, ncclFloat32, 0, s.comms[size_t(r)], rs));
+            }
+        } catch (...) {
+            (void)R.group_end();
+            throw;
+        }
+        NCCL_TRY(R.group_end());
+        for (auto& rep : s.replicas) {
+            set_device(*rep);
+            HIP_TRY(hipEventRecord(rep->done, rep->stream));
+        }
+        set_device(s);
+    }
     for (auto& R : s.replicas) HIP_TRY(hipStreamWaitEvent(st, R->done, 0));
     mcpt::GatherParams g{};
     g.src = static_cast<const float4*>(s.gather);
@@ -1332,18 +1504,24 @@ int mcpt_scene_reserve(mcpt_scene* s, const mcpt_render_params* p) {
             return MCPT_OK;
         }
         const int n = 1 + static_cast<int>(s->replicas.size());
+        const bool use_rccl = p->gather == MCPT_GATHER_RCCL;
+        set_device(*s);
+        const uint64_t slot = multi_slot(make_plan(*s, p), p, n);
         for (int r = 0; r < n; ++r) {
             mcpt_render_params pr = *p;
             pr.shard_count = n; pr.shard_index = r; pr.packed = 1;
             mcpt_scene& sc = r ? *s->replicas[size_t(r - 1)] : *s;
             reserve(sc, &pr);
-            if (r) ensure_buf(sc.ws.fb, sc.ws.fb_bytes, size_t(mcpt_shard_pixel_count(&pr)) * 16);
+            if (r) ensure_buf(sc.ws.fb, sc.ws.fb_bytes, use_rccl ? size_t(slot) * 16
+                                                                  : size_t(mcpt_shard_pixel_count(&pr)) * 16);
         }
         set_device(*s);
         // the gather buffer: n slots of the largest shard (shard 0 owns the most tiles)
-        mcpt_render_params p0 = *p;
-        p0.shard_count = n; p0.shard_index = 0; p0.packed = 1;
-        ensure_buf(s->gather, s->gather_bytes, size_t(n) * size_t(mcpt_shard_pixel_count(&p0)) * 16);
+        ensure_buf(s->gather, s->gather_bytes, size_t(n) * size_t(slot) * 16);
+        if (use_rccl) {   // the communicators and rank 0's send buffer exist before any capture
+            ensure_comms(*s);
+            ensure_buf(s->gather_send, s->gather_send_bytes, size_t(slot) * 16);
+        }
         if (!s->start) HIP_TRY(hipEventCreateWithFlags(&s->start, hipEventDisableTiming));
         return MCPT_OK;
     });

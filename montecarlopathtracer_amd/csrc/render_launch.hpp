@@ -25,6 +25,13 @@
 
 namespace mcpt {
 
+// 1: images with 8-B node words (LDS scenes) order their sibling pairs in
+// two-level groups and mark the group roots (bit 29 of an inner node word;
+// trace_device.hpp descend_steps, capi.cpp device_order_groups)
+#ifndef MCPT_KD_GROUPS
+#define MCPT_KD_GROUPS 1
+#endif
+
 constexpr int kLdsBlock = 1024;          // in-LDS variant: one 16-wave workgroup per CU
 constexpr int kGlobalBlock = 256;        // global variant
 constexpr int kGlobalBlocksPerCu = 4;

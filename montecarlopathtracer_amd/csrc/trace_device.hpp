@@ -294,6 +294,9 @@ __device__ __forceinline__ float4 ld_tri(const float4* __restrict__ p) {
 #ifndef MCPT_DESCENT_CAP_GLOBAL
 #define MCPT_DESCENT_CAP_GLOBAL 5                // global-memory scenes (C4: 5 > 4)
 #endif
+#ifndef MCPT_GROUP_CAP
+#define MCPT_GROUP_CAP 2                         // node groups: loop iterations of <= 2 levels each
+#endif
 // Child-box cull (scenes in global memory): each sibling-pair record also
 // carries both children's KD boxes (the node region clipped to its
 // triangles' bounds, KDTree.hpp:154-155) as fp16 rounded outward
@@ -379,10 +382,77 @@ __device__ __forceinline__ bool pop_entry(RayState& r, uint4* st, int stride, ui
     return !(r.best <= r.tmin * kEpsLo);
 }
 
+// Two-level node groups (scenes whose image has 8-B node words, i.e. LDS
+// scenes; MCPT_KD_GROUPS): the inner nodes at even depth are group roots
+// (kGroupBit in the node word).  A root's sibling pair is followed in the
+// image by the pairs of its inner children -- the left child's first -- so one
+// 48-B read at the root's `left` (three ds_read_b128 issued together) brings
+// both levels below it, and one loop iteration takes two steps of the walk:
+// one LDS round trip and one loop branch per two levels.  The walk, its
+// order, intervals, pushes and counters are the per-level walk's (each level
+// counts as an inner visit); only the device image's pair order changes (the
+// host builds it, capi.cpp device_order_groups).  A popped entry whose node
+// is an odd-depth child (pushed at a group's first level) takes one level,
+// its children are group roots again.
+constexpr uint32_t kGroupBit = 1u << 29;
+constexpr uint32_t kLeftMask = MCPT_KD_GROUPS ? 0x1FFFFFFFu : 0x3FFFFFFFu;   // inner node word: child pair index
+
+// One inner-node step of the ordered walk on 8-B node words: the node in
+// (w0, w1), its children's pair record pr; the far child is pushed when both
+// are needed, (w0, w1) advance to the child entered.
+template <int S, bool COUNT>
+__device__ __forceinline__ void kd_step(RayState& r, uint32_t& w0, uint32_t& w1, const uint4 pr, uint4* st, int stride,
+                                        uint4* __restrict__ spill, uint32_t spill_stride, Counters& c) {
+    const int32_t U = stride * 16;            // one stack position (see slot_of)
+    const int a = (int)(w0 >> 30);
+    const float sv = __uint_as_float(w1);
+    const float oa = sel3(a, r.o.x, r.o.y, r.o.z);
+    const float ia = sel3(a, r.ix, r.iy, r.iz);
+    const float t = (sv - oa) * ia;
+    // near side: below the plane, or on it and heading down; pp = ray inside
+    // the plane (both children).  Only an origin exactly on the plane needs
+    // the direction, so its select and tests sit in a rarely taken branch.
+    bool below = oa < sv, pp = false;
+    if (__builtin_expect(oa == sv, 0)) {
+        const float da = sel3(a, r.d.x, r.d.y, r.d.z);
+        below = da <= 0.0f;
+        pp = da == 0.0f;
+    }
+    // if/else chain of the oracle, evaluated branch-free
+    const float te = t * kEpsHi;
+    const bool no = !(t > 0.0f) | (t > r.tmax);                 // near child only
+    const bool fo = te < r.tmin;                                // far child only
+    const bool go_far = !pp & !no & fo;
+    const bool both = !pp & !no & !fo;                          // push far, go near
+    const bool push_it = pp | both;
+    const uint32_t f0 = below ? pr.z : pr.x, f1 = below ? pr.w : pr.y;     // far child record
+    if (push_it) {
+        // pp ? tmin : max(t, tmin) without the select: a pp lane's t is
+        // (+0) * (+-inf) = NaN (da = +-0, oa == sv), and max returns tmin
+        const float plo = max_qnan(t, r.tmin);
+        lds_uint4* slot = slot_of<S>(st, stride, r.sp);
+        if (r.sp - r.lo == S * U) {       // LDS part full: its oldest entry (same slot) to memory
+            spill[((uint32_t)r.lo / (uint32_t)U) * spill_stride] = ld4(slot);
+            r.lo += U;
+            if constexpr (COUNT) c.spills++;
+        }
+        st4(slot, make_uint4(f0, f1, __float_as_uint(plo), __float_as_uint(r.tmax)));
+        r.sp += U;
+        r.tmax = min_qnan(te, r.tmax);    // here push_it & !pp == both; te = NaN for pp
+    }
+    // the child entered: the near one, or the far one when go_far (the
+    // left record when below != go_far) -- two selects, not four
+    const bool enter_left = below != go_far;
+    w0 = enter_left ? pr.x : pr.z;
+    w1 = enter_left ? pr.y : pr.w;
+}
+
 // Descent of a ray between leaves: at most `cap` inner-node steps (the node
 // record and interval stay in the ray state); 0 = cap reached mid-descent,
 // 1 = a leaf reached (its refs in [lpos, lend)), 2 = the walk ended (a
-// global-memory scene's box cull popped past the last interval).
+// global-memory scene's box cull popped past the last interval).  With node
+// groups (8-B node words, MCPT_KD_GROUPS) `cap` counts loop iterations of up
+// to two levels each.
 // COUNT = false (lean renders): the counters are compiled out.
 template <int S, bool BOXES = false, bool COUNT = true>
 __device__ __forceinline__ int descend_steps(RayState& r, const uint2* __restrict__ nodes1, uint4* st, int stride,
@@ -394,6 +464,30 @@ __device__ __forceinline__ int descend_steps(RayState& r, const uint2* __restric
     uint32_t& w0 = r.nw0;
     uint32_t& w1 = r.nw1;
     int steps = 0;
+    if constexpr (!BOXES && MCPT_KD_GROUPS) {
+        while ((w0 >> 30) != 3u) {
+            if (steps == cap) return 0;       // resume next call
+            steps++;
+            if constexpr (COUNT) c.inner++;
+            MCPT_LANE_USE(desc_w, desc_l, lu);
+            const uint32_t left = w0 & kLeftMask;
+            const bool grp = (w0 & kGroupBit) != 0u;
+            // the node's pair and the two pairs after it (its children's, if it
+            // is a group root), requested together
+            const uint4* g = reinterpret_cast<const uint4*>(nodes1 + left);
+            const uint4 p0 = g[0], p1 = g[1], p2 = g[2];
+            kd_step<S, COUNT>(r, w0, w1, p0, st, stride, spill, spill_stride, c);
+            if (grp & ((w0 >> 30) != 3u)) {   // a group root's inner child: its pair is in the group
+                if constexpr (COUNT) c.inner++;
+                const uint4 pc = (w0 & kLeftMask) == left + 2u ? p1 : p2;
+                kd_step<S, COUNT>(r, w0, w1, pc, st, stride, spill, spill_stride, c);
+            }
+        }
+        if constexpr (COUNT) c.leaf++;
+        r.lpos = w0 & 0x3FFFFFFFu;
+        r.lend = r.lpos + w1;
+        return 1;
+    }
     while ((w0 >> 30) != 3u) {
         if (steps == cap) return 0;           // resume next call
         steps++;
@@ -490,7 +584,9 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
     const int32_t U = stride * 16;            // one stack position (see slot_of)
     if (r.lpos == r.lend) {                   // between leaves: descend
         const int k = descend_steps<S, BOXES, COUNT>(r, nodes1, st, stride, spill, spill_stride, c, pairs,
-                                                      CAP > 0 ? CAP : BOXES ? MCPT_DESCENT_CAP_GLOBAL : MCPT_DESCENT_CAP
+                                                      CAP > 0 ? CAP : BOXES ? MCPT_DESCENT_CAP_GLOBAL
+                                                                            : (MCPT_KD_GROUPS ? MCPT_GROUP_CAP
+                                                                                              : MCPT_DESCENT_CAP)
                                                       MCPT_LU_ARG);
         if (k == 0) return false;
         if (k == 2) return true;

@@ -278,6 +278,10 @@ struct ClassBuf {
 #ifndef MCPT_WF_DESCENT_CAP_GLOBAL
 #define MCPT_WF_DESCENT_CAP_GLOBAL MCPT_DESCENT_CAP_GLOBAL
 #endif
+#ifndef MCPT_WF_GROUP_CAP
+#define MCPT_WF_GROUP_CAP 3                      // node groups (LDS scenes): iterations of <= 2 levels
+#endif
+constexpr int kWfLdsCap = MCPT_KD_GROUPS ? MCPT_WF_GROUP_CAP : MCPT_WF_DESCENT_CAP;
 
 #ifndef MCPT_WF_GEO_LDS
 #define MCPT_WF_GEO_LDS 1
@@ -389,7 +393,7 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
             }
 #endif
             if (mode == kTrav) {
-                if (trav_iter<S, !IN_LDS, COUNT, IN_LDS, IN_LDS ? MCPT_WF_DESCENT_CAP : MCPT_WF_DESCENT_CAP_GLOBAL>(r, tris, nodes, leafs, st, BLOCK, spill, spill_stride, c MCPT_LU_ARG,
+                if (trav_iter<S, !IN_LDS, COUNT, IN_LDS, IN_LDS ? kWfLdsCap : MCPT_WF_DESCENT_CAP_GLOBAL>(r, tris, nodes, leafs, st, BLOCK, spill, spill_stride, c MCPT_LU_ARG,
                                                  pairs))
                     mode = kReady;
             }
@@ -613,8 +617,8 @@ __global__ void __launch_bounds__(BLOCK) wf_extend_primary(const KernelParams kp
                 if ((w0 >> 30) != 3u) {
                     // ---- inner node: each lane's step of isect_kd_ordered ----
                     if constexpr (COUNT) c.inner += active ? 1u : 0u;
-                    const uint32_t left = w0 & 0x3FFFFFFFu;
-                    const uint4 pr = *reinterpret_cast<const uint4*>(nodes + left);
+                    const uint32_t left = w0 & kLeftMask;     // (one level per node: a group's
+                    const uint4 pr = *reinterpret_cast<const uint4*>(nodes + left);   // first pair)
                     const int a = (int)(w0 >> 30);
                     const float sv = __uint_as_float(w1);
                     const float oa = sel3(a, eye.x, eye.y, eye.z);

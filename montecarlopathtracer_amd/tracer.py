@@ -152,6 +152,7 @@ class ObjModel:
 
 PIPELINES = {"megakernel": _capi.PIPELINE_MEGAKERNEL, "wavefront": _capi.PIPELINE_WAVEFRONT}
 MODES = {"cvmctracer": _capi.MODE_CVMCTRACER, "quinengine": _capi.MODE_QUINENGINE}
+GATHERS = {"peer": _capi.GATHER_PEER, "rccl": _capi.GATHER_RCCL}
 
 
 @dataclass
@@ -189,6 +190,7 @@ class RenderParams:
     tail_units: int = 0               # megakernel: exact tail-split units (> 0 overrides)
     wf_mem_limit: int = 0             # wavefront queue memory budget in bytes (0: 90% of free)
     force_peer_copy: bool = False     # multi-device: hipMemcpyPeerAsync also between same-device replicas
+    gather: str = "peer"              # multi-device shards to devices[0]: "peer" copies or "rccl" (ncclGather)
 
     @staticmethod
     def for_scene(scene_id: int, **kw) -> "RenderParams":
@@ -232,6 +234,9 @@ class RenderParams:
         p.ready_thresh, p.tail_units_per_lane = int(self.ready_thresh), int(self.tail_units_per_lane)
         p.tail_units, p.wf_mem_limit = int(self.tail_units), int(self.wf_mem_limit)
         p.force_peer_copy = 1 if self.force_peer_copy else 0
+        if self.gather not in GATHERS:
+            raise ValueError(f"gather must be one of {sorted(GATHERS)}")
+        p.gather = GATHERS[self.gather]
         return p
 
     def output_pixels(self) -> int:
