@@ -340,6 +340,30 @@ def host_cores() -> int:
     return max(1, min(n, int(os.environ.get("OMP_NUM_THREADS", "16"))))
 
 
+def c4_line(args) -> dict:
+    """BASELINE configs[3] (C4: the seeded 70k-triangle mesh in scene01's box,
+    1024x1024 @ 1024 spp, scene image in global memory with the child-box
+    cull) timed the same way, in a child process of this bench (its own GPU
+    context; this process's workspace stays allocated beside it)."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--scene", "cornell_bunny70k", "--no-c4", "--no-alt",
+           "--no-cpu-baseline", "--steps", str(args.steps), "--warmup", str(args.warmup),
+           "--width", str(args.width), "--height", str(args.height), "--spp", str(args.spp),
+           "--spp-chunk", str(args.spp_chunk), "--pipeline", args.pipeline] + (["--no-pmc"] if args.no_pmc else []) + \
+        (["--keep-pmc", os.path.join(args.keep_pmc, "c4")] if args.keep_pmc else [])
+    env = dict(os.environ)
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
+    except subprocess.TimeoutExpired:
+        return {"error": "C4 child timed out"}
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"error": f"C4 child rc {r.returncode}: {r.stderr[-400:]}"}
+    return json.loads(lines[-1])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -374,6 +398,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = this process's CPU share (<= 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-c4", action="store_true",
+                    help="N = 1: skip the C4 line (BASELINE configs[3], the 70k-triangle mesh in the Cornell box, "
+                         "same pipeline, steps and PMC roofline) reported under extra_lines.c4")
     ap.add_argument("--counting", action="store_true", help="time the counting megakernel instead of the lean one")
     ap.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 PMC passes (HBM bytes, VALU issue)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)   # one render under rocprofv3
@@ -556,7 +583,7 @@ def main():
                 # rank 0's shard: its share of the frame's counts (interleaved tiles, ~1/N)
                 lb = lds_block(ext.pop("lds_counters", {}), cus,
                                {k: per_launch[k] / n_gpus for k in ("inner_visits", "leaf_refs", "tri_tests")})
-                if lb:
+                if lb and st["variant"] == 4:    # scene image in LDS (the global variant's LDS holds only stacks)
                     lb["kernel"] = "wf_extend, run alone"
                     roof["lds"] = lb
                 roof.update(binding_of(roof))
@@ -646,6 +673,8 @@ def main():
             "cpu_baseline": None,
             "other_pipeline": alt,
         }
+        if n_gpus == 1 and not args.no_c4 and args.scene == "scene01":
+            line["extra_lines"] = {"c4": c4_line(args)}
         if n_gpus == 1 and not args.no_cpu_baseline:
             # the GPU's own C1 frame, for the ray-count check of the CPU run
             s1 = scene if args.scene == "scene01" else M.Scene(M.ObjModel(M.scene_path("scene01")))

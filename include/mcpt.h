@@ -86,7 +86,7 @@ typedef struct {
     int32_t shard_index;
     int32_t packed;             /* 1: write owned tiles packed (tile-major) instead of row-major */
     int32_t pipeline;           /* MCPT_PIPELINE_*: megakernel (default) or wavefront; same image */
-    uint32_t wf_batch;          /* wavefront: max paths per batch and stream (160 B of device memory
+    uint32_t wf_batch;          /* wavefront: max paths per batch and stream (120 B of device memory
                                    each), 0 = automatic: LDS scenes 2^28 on one or two streams,
                                    2^27 on three or more; global-memory scenes 2^28 on one stream,
                                    2^27 on more; a default batch is also capped at work / streams
@@ -320,7 +320,7 @@ int mcpt_intersect(mcpt_scene* s, int64_t n, const float* o, const float* d, flo
  * (required before hipGraph capture).  Megakernel workspace per render:
  * partial sums 16 B x pixels x ceil(spp/chunk), the tail-split buffer (16 B
  * per sample of the last ~4 units per lane) and the stack spill area (32 x
- * 16 B per lane); wavefront: 160 B per path of the batch.                    */
+ * 16 B per lane); wavefront: 120 B per path of the batch (160 with wf_sort).  */
 int mcpt_scene_reserve(mcpt_scene* s, const mcpt_render_params* p);
 /* The scheduling a render of p would use and its memory (no allocation, no launch). */
 int mcpt_plan_query(mcpt_scene* s, const mcpt_render_params* p, mcpt_plan_info* out);

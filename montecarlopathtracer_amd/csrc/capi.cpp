@@ -523,22 +523,28 @@ int wavefront_streams(const mcpt_scene& s, uint64_t work, const mcpt_render_para
 }
 
 // Device memory of one stream's wavefront workspace for batches of `cap`
-// paths (prepare_wavefront carves it): two ray queues of four float4 streams,
-// radiance, four class lists (160 B per slot), per-bounce counters.  Segments
-// hold whole path groups (2^group_shift paths: 64 for LDS scenes, up to 2^14
-// for global-memory ones): up to one group of slots per segment beyond the paths.
+// paths (prepare_wavefront carves it): two ray queues, radiance, per-bounce
+// counters; the material sort also four class lists.  A queue is three float4
+// streams (origin + path id, direction + depth, throughput + RNG state) and
+// the hit stream: 4-B triangle ids in queue order (wavefront.hip kQHIT), 16-B
+// hit records for the material sort.  Queue order: 3 x 16 + 4 B per slot and
+// queue, 120 B per path with the radiance (the sort: 160 B).  Segments hold
+// whole path groups (2^group_shift paths: 64 for LDS scenes, up to 2^14 for
+// global-memory ones): up to one group of slots per segment beyond the paths.
 struct WfLayout {
-    size_t cap_slots, f4, need;
+    size_t cap_slots, f4, queue, need;
 };
 WfLayout wf_layout(const mcpt_scene& s, const Plan& pl, uint64_t cap) {
     const mcpt::KernelParams& kp = pl.kp;
     const size_t nseg = static_cast<size_t>(mcpt::wavefront_segments(s.gpu, s.cus));
     const size_t queries = kp.mode == MCPT_MODE_QUINENGINE ? 3 * size_t(kp.max_depth) + 1 : size_t(kp.max_depth) + 1;
     const size_t bounces = (queries + 1) * nseg;
+    auto al256 = [](size_t x) { return (x + 255) & ~size_t(255); };
     WfLayout l;
     l.cap_slots = size_t(cap) + (nseg << pl.wf_group_shift);
     l.f4 = l.cap_slots * 16;
-    l.need = (2 * 4 * l.f4 + l.f4 + 4 * l.cap_slots * 4 + bounces * sizeof(mcpt::WfCounters) + 256 + 255) & ~size_t(255);
+    l.queue = al256(pl.wf_sort ? 4 * l.f4 : 3 * l.f4 + 4 * l.cap_slots);
+    l.need = al256(2 * l.queue + l.f4 + (pl.wf_sort ? 4 * l.cap_slots * 4 : 0) + bounces * sizeof(mcpt::WfCounters) + 256);
     return l;
 }
 
@@ -640,7 +646,7 @@ Plan make_plan(const mcpt_scene& s, const mcpt_render_params* p) {
     pl.tail_exact = p->tail_units;
     pl.wf_mem_limit = p->wf_mem_limit;
     {
-        // default batch: big (160 B of queues per path and stream; fewer launches,
+        // default batch: big (120 B of queues per path and stream; fewer launches,
         // shorter relative tails).  One stream: C2 2^24 5.59, 2^25 6.43, 2^26 7.07,
         // 2^27 7.31, 2^28 7.24; C4 (256 spp) 2^24 2.90, 2^26 3.45, 2^28 4.31 G
         // rays/s.  Global-memory scenes on 4 streams: 2^27 each (see wavefront_streams);
@@ -658,7 +664,7 @@ Plan make_plan(const mcpt_scene& s, const mcpt_render_params* p) {
         if (!p->wf_batch && nstr > 1) cap = std::min<uint64_t>(cap, (work + nstr - 1) / nstr);
         cap = std::max<uint64_t>(cap, chunk);                        // at least one pixel per batch
         cap = std::min<uint64_t>(cap, work);
-        cap = std::min<uint64_t>(cap, uint64_t(1) << 28);               // u32 slot arithmetic; 160 B per path
+        cap = std::min<uint64_t>(cap, uint64_t(1) << 28);               // u32 slot arithmetic; 120 B per path
         pl.wf_capacity = static_cast<uint32_t>(cap);
         pl.wf_batch_explicit = p->wf_batch != 0;
     }
@@ -759,10 +765,13 @@ void prepare_wavefront(mcpt_scene& s, const Plan& pl, int sets, mcpt::WfParams* 
         char* b = static_cast<char*>(s.ws.wf) + size_t(h) * l.need;
         mcpt::WfParams& w = out[h];
         std::memset(&w, 0, sizeof w);
-        w.q[0] = reinterpret_cast<float4*>(b); b += 4 * l.f4;
-        w.q[1] = reinterpret_cast<float4*>(b); b += 4 * l.f4;
+        w.q[0] = reinterpret_cast<float4*>(b); b += l.queue;
+        w.q[1] = reinterpret_cast<float4*>(b); b += l.queue;
         w.radiance = reinterpret_cast<float4*>(b); b += l.f4;
-        w.cls_list = reinterpret_cast<uint32_t*>(b); b += 4 * l.cap_slots * 4;
+        if (pl.wf_sort) {
+            w.cls_list = reinterpret_cast<uint32_t*>(b);
+            b += 4 * l.cap_slots * 4;
+        }
         w.cnt = reinterpret_cast<mcpt::WfCounters*>(b);
         w.capacity = pl.wf_capacity;                   // paths per batch (pid range)
         w.slot_stride = static_cast<uint32_t>(l.cap_slots);

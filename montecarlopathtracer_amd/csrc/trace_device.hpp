@@ -294,6 +294,9 @@ __device__ __forceinline__ float4 ld_tri(const float4* __restrict__ p) {
 #ifndef MCPT_DESCENT_CAP_GLOBAL
 #define MCPT_DESCENT_CAP_GLOBAL 5                // global-memory scenes (C4: 5 > 4)
 #endif
+#ifndef MCPT_GROUP_LOAD
+#define MCPT_GROUP_LOAD 0                        // 1: a node group's child pairs read by roots only
+#endif
 #ifndef MCPT_GROUP_CAP
 #define MCPT_GROUP_CAP 2                         // node groups: loop iterations of <= 2 levels each
 #endif
@@ -475,7 +478,16 @@ __device__ __forceinline__ int descend_steps(RayState& r, const uint2* __restric
             // the node's pair and the two pairs after it (its children's, if it
             // is a group root), requested together
             const uint4* g = reinterpret_cast<const uint4*>(nodes1 + left);
-            const uint4 p0 = g[0], p1 = g[1], p2 = g[2];
+            const uint4 p0 = g[0];
+#if MCPT_GROUP_LOAD
+            uint4 p1 = make_uint4(0, 0, 0, 0), p2 = p1;
+            if (grp) {                        // (only a group root's read brings its children's pairs)
+                p1 = g[1];
+                p2 = g[2];
+            }
+#else
+            const uint4 p1 = g[1], p2 = g[2];
+#endif
             kd_step<S, COUNT>(r, w0, w1, p0, st, stride, spill, spill_stride, c);
             if (grp & ((w0 >> 30) != 3u)) {   // a group root's inner child: its pair is in the group
                 if constexpr (COUNT) c.inner++;

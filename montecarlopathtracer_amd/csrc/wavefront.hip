@@ -63,8 +63,8 @@ __device__ __forceinline__ float opaque(float x) {
 }
 __device__ __forceinline__ float4 pack(V3 v, uint32_t w) { return make_float4(v.x, v.y, v.z, __uint_as_float(w)); }
 
-// Queue layout: field k of slot j (0 {o, pid}, 1 {d, depth}, 2 hit {t, beta,
-// gamma, htri}, 3 {throughput, rng}).  SoA (default): four float4 streams of
+// Queue layout: field k of slot j (kQO {o, pid}, kQD {d, depth}, kQPS
+// {throughput, rng}, kQHIT hit {t, beta, gamma, htri} or the 4-B id).  SoA (default): four float4 streams of
 // slot_stride entries each -- extend's ray reads and hit writes are dense
 // 16-B lane streams; AoS: one 64-B record per slot.
 #ifndef MCPT_WF_SOA
@@ -85,6 +85,10 @@ __device__ __forceinline__ size_t qf(uint32_t slot, uint32_t k, uint32_t stride)
     return 4u * (size_t)slot + k;
 #endif
 }
+// queue streams: origin + path id, direction + depth, throughput + RNG state,
+// hit (last: in queue order it holds only 4-B triangle ids, MCPT_WF_HIT_ID, so
+// the queue is 3 x 16 + 4 B per slot; the material sort keeps 16-B hit records)
+constexpr uint32_t kQO = 0, kQD = 1, kQPS = 2, kQHIT = 3;
 __device__ __forceinline__ V3 xyz(float4 v) { return v3(v.x, v.y, v.z); }
 
 // Queue streams are touched once per bounce: MCPT_WF_NT marks the streaming
@@ -179,6 +183,7 @@ __host__ __device__ __forceinline__ bool implicit0(const KernelParams& kp, const
 #define MCPT_WF_HIT_ID 1
 #endif
 static_assert(MCPT_WF_SOA || !MCPT_WF_HIT_ID, "hit ids use the SoA hit stream");
+static_assert(MCPT_WF_HIT_ID && MCPT_WF_SOA, "capi.cpp wf_layout: queue-order queues hold 4-B hit ids, SoA");
 
 // ---- generate: primary rays of the batch (CUTracer.cu:186-211) -------------
 // Paths go to segments in groups of 2^group_shift (64 = one 8x8 tile of one
@@ -209,13 +214,13 @@ __global__ void __launch_bounds__(kGenBlock) wf_generate(const KernelParams kp, 
             else
                 primary_ray(kp, pix, px, py, wf.s_begin + s_local, sd, d);
             if (!implicit0(kp, wf))
-                stq(&wf.q[0][qf(slot, 3, wf.slot_stride)], make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(sd)));
+                stq(&wf.q[0][qf(slot, kQPS, wf.slot_stride)], make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(sd)));
             c.paths++;
             c.rays++;
             depth = 0;
         }
-        if (!(MCPT_WF_IMPLICIT0 >= 2 && implicit0(kp, wf))) stq(&wf.q[0][qf(slot, 0, wf.slot_stride)], pack(o, pid));
-        stq(&wf.q[0][qf(slot, 1, wf.slot_stride)], pack(d, depth));
+        if (!(MCPT_WF_IMPLICIT0 >= 2 && implicit0(kp, wf))) stq(&wf.q[0][qf(slot, kQO, wf.slot_stride)], pack(o, pid));
+        stq(&wf.q[0][qf(slot, kQD, wf.slot_stride)], pack(d, depth));
     }
     flush_counters(c, kp.stats);
 }
@@ -377,9 +382,9 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
     // MCPT_WF_IMPLICIT0 >= 2: bounce 0's origins are the eye (CV mode), not read
     const bool eye0 = MCPT_WF_IMPLICIT0 >= 2 && wf.bounce == 0 && implicit0(kp, wf);
     const float4 eye4 = make_float4(kp.eye[0], kp.eye[1], kp.eye[2], 0.0f);
-    auto ld_o = [&](uint32_t sl) { return eye0 ? eye4 : ldq(&qb[qf(seg0 + sl, 0, qs)]); };
-    if (slot < count) start(ld_o(slot), ldq(&qb[qf(seg0 + slot, 1, qs)]));
-    if (nslot < count) { no4 = ld_o(nslot); nd4 = ldq(&qb[qf(seg0 + nslot, 1, qs)]); }
+    auto ld_o = [&](uint32_t sl) { return eye0 ? eye4 : ldq(&qb[qf(seg0 + sl, kQO, qs)]); };
+    if (slot < count) start(ld_o(slot), ldq(&qb[qf(seg0 + slot, kQD, qs)]));
+    if (nslot < count) { no4 = ld_o(nslot); nd4 = ldq(&qb[qf(seg0 + nslot, kQD, qs)]); }
     WF_STAMP(tm_setup);
     for (;;) {
         // ---- traversal burst until enough lanes are done ---------------------
@@ -433,11 +438,11 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
             start(no4, nd4);
             if (nslot >= count) mode = kDead;
             if constexpr (MCPT_WF_HIT_ID && !SORT)   // (r holds the next ray by now: the id from hrec)
-                reinterpret_cast<int32_t*>(qb + qf(0, 2, qs))[seg0 + fslot] = __float_as_int(hrec.w);
+                reinterpret_cast<int32_t*>(qb + qf(0, kQHIT, qs))[seg0 + fslot] = __float_as_int(hrec.w);
             else if constexpr ((MCPT_WF_NT & 4) != 0 || (!IN_LDS && MCPT_WF_NT_HIT_GLOBAL))
-                stq_nt(&qb[qf(seg0 + fslot, 2, qs)], hrec);
+                stq_nt(&qb[qf(seg0 + fslot, kQHIT, qs)], hrec);
             else
-                qb[qf(seg0 + fslot, 2, qs)] = hrec;
+                qb[qf(seg0 + fslot, kQHIT, qs)] = hrec;
         }
         if constexpr (SORT) {
 #pragma unroll
@@ -449,7 +454,7 @@ __global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const 
         const uint32_t ns = cur_chunk.take(want, lcnt + 4);
         if (want) {
             nslot = ns;
-            if (nslot < count) { no4 = ld_o(nslot); nd4 = ldq(&qb[qf(seg0 + nslot, 1, qs)]); }
+            if (nslot < count) { no4 = ld_o(nslot); nd4 = ldq(&qb[qf(seg0 + nslot, kQD, qs)]); }
         }
         WF_STAMP(tm_hand);
         if (!__ballot(mode != kDead)) break;
@@ -567,7 +572,7 @@ __global__ void __launch_bounds__(BLOCK) wf_extend_primary(const KernelParams kp
     // The hits of a group are stored one group later, after the wait for the
     // next directions: a store issued at the end of the walk would make that
     // wait (vmcnt counts stores too) wait for its acknowledgement.
-    int32_t* const hq = reinterpret_cast<int32_t*>(qb + qf(0, 2, qs)) + seg0;
+    int32_t* const hq = reinterpret_cast<int32_t*>(qb + qf(0, kQHIT, qs)) + seg0;
     // the primary ray of local slot j: direction and depth (kNoRay: a pixel
     // outside the image, an empty slot)
     auto dir_of = [&](uint32_t j) {
@@ -586,7 +591,7 @@ __global__ void __launch_bounds__(BLOCK) wf_extend_primary(const KernelParams kp
             }
             return d4;
         } else {
-            return ldq(&qb[qf(seg0 + j, 1, qs)]);
+            return ldq(&qb[qf(seg0 + j, kQD, qs)]);
         }
     };
     uint32_t base = take_group();
@@ -762,7 +767,7 @@ __global__ void __launch_bounds__(kShadeBlock) wf_shade(const KernelParams kp, c
         const uint32_t start = k == 1u ? 0u : (k == 2u ? p1 : (k == 3u ? p2 : p3));
         const uint32_t slot = wf.cls_list[(size_t)k * wf.slot_stride + seg0 + (i - start)];
         const size_t js = seg0 + slot;
-        const float4 o4 = qb[qf(js, 0, qs)], d4 = qb[qf(js, 1, qs)], h = qb[qf(js, 2, qs)], ps = qb[qf(js, 3, qs)];
+        const float4 o4 = qb[qf(js, kQO, qs)], d4 = qb[qf(js, kQD, qs)], h = qb[qf(js, kQHIT, qs)], ps = qb[qf(js, kQPS, qs)];
         const uint32_t pid = __float_as_uint(o4.w);
         const uint32_t depth = __float_as_uint(d4.w);
         const int32_t htri = __float_as_int(h.w);
@@ -791,19 +796,19 @@ __global__ void __launch_bounds__(kShadeBlock) wf_shade(const KernelParams kp, c
             if (qe && (int32_t)depth >= kp.max_depth && !qe_roulette(sd, color)) {
                 // killed by the roulette: zero radiance, an empty slot in queue b+1
                 wf.radiance[pid] = make_float4(0, 0, 0, 0);
-                qb2[qf(ji, 0, qs)] = pack(v3(0, 0, 0), pid);
-                qb2[qf(ji, 1, qs)] = pack(v3(0, 0, 0), kNoRay);
-                qb2[qf(ji, 2, qs)] = make_float4(0, 0, 0, 0);
-                qb2[qf(ji, 3, qs)] = make_float4(0, 0, 0, 0);
+                qb2[qf(ji, kQO, qs)] = pack(v3(0, 0, 0), pid);
+                qb2[qf(ji, kQD, qs)] = pack(v3(0, 0, 0), kNoRay);
+                qb2[qf(ji, kQHIT, qs)] = make_float4(0, 0, 0, 0);
+                qb2[qf(ji, kQPS, qs)] = make_float4(0, 0, 0, 0);
             } else {
                 c.shades++;
                 const GpuGeom& gm = geoms[__float_as_uint(tris[htri + 1].w)];
                 V3 o = xyz(o4), d = xyz(d4);
                 if (qe) scatter<true>(gm, sc.normals, htri, h.y, h.z, h.x, 0, sd, color, o, d);
                 else scatter<false>(gm, sc.normals, htri, h.y, h.z, h.x, kp.fresnel_kd, sd, color, o, d);
-                qb2[qf(ji, 0, qs)] = pack(o, pid);
-                qb2[qf(ji, 1, qs)] = pack(d, depth + 1u);
-                qb2[qf(ji, 3, qs)] = pack(color, sd);
+                qb2[qf(ji, kQO, qs)] = pack(o, pid);
+                qb2[qf(ji, kQD, qs)] = pack(d, depth + 1u);
+                qb2[qf(ji, kQPS, qs)] = pack(color, sd);
                 c.rays++;
             }
         }
@@ -856,10 +861,10 @@ __global__ void __launch_bounds__(BLOCK) wf_shade_slots(const KernelParams kp, c
         if (i < total) {
             const size_t js = seg0 + i;
 #if MCPT_WF_HIT_ID
-            const int32_t htri = reinterpret_cast<const int32_t*>(qb + qf(0, 2, qs))[js];
+            const int32_t htri = reinterpret_cast<const int32_t*>(qb + qf(0, kQHIT, qs))[js];
             float4 h = make_float4(0, 0, 0, 0);
 #else
-            const float4 h = ldq(&qb[qf(js, 2, qs)]);
+            const float4 h = ldq(&qb[qf(js, kQHIT, qs)]);
             const int32_t htri = __float_as_int(h.w);
 #endif
             float4 o4, d4, ps;
@@ -880,9 +885,9 @@ __global__ void __launch_bounds__(BLOCK) wf_shade_slots(const KernelParams kp, c
                     ps.w = __uint_as_float(sd0);
                 }
             } else {
-                o4 = ldq(&qb[qf(js, 0, qs)]);
-                d4 = ldq(&qb[qf(js, 1, qs)]);
-                ps = ldq(&qb[qf(js, 3, qs)]);
+                o4 = ldq(&qb[qf(js, kQO, qs)]);
+                d4 = ldq(&qb[qf(js, kQD, qs)]);
+                ps = ldq(&qb[qf(js, kQPS, qs)]);
             }
             pid = __float_as_uint(o4.w);
             depth = __float_as_uint(d4.w);
@@ -930,9 +935,9 @@ __global__ void __launch_bounds__(BLOCK) wf_shade_slots(const KernelParams kp, c
             b0 = lane_bcast(b0, leader);
             if (cont) {
                 const size_t ji = seg0 + b0 + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-                stq(&qb2[qf(ji, 0, qs)], pack(o, pid));
-                stq(&qb2[qf(ji, 1, qs)], pack(d, depth + 1u));
-                stq(&qb2[qf(ji, 3, qs)], pack(color, sd));
+                stq(&qb2[qf(ji, kQO, qs)], pack(o, pid));
+                stq(&qb2[qf(ji, kQD, qs)], pack(d, depth + 1u));
+                stq(&qb2[qf(ji, kQPS, qs)], pack(color, sd));
             }
         }
     }

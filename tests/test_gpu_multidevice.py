@@ -160,7 +160,11 @@ def test_plan_query_reports_the_schedule(mcpt, devices):
     wf = scene.plan(mcpt.RenderParams(pipeline="wavefront", **c2))
     assert (wf["pipeline"], wf["variant"], wf["wf_streams"], wf["wf_batch"]) == (1, 4, 3, 1 << 27)
     assert wf["wf_refill"] == 16 and wf["wf_group_shift"] == 6 and wf["work_paths"] == 1 << 30
-    assert 3 * 160 * (1 << 27) <= wf["workspace_bytes"] < wf["device_free_bytes"]
+    # queue order: 2 queues x (3 x 16 + 4 B) + 16 B of radiance = 120 B per path and stream
+    assert 3 * 120 * (1 << 27) <= wf["wf_queue_bytes"] < 3 * 121 * (1 << 27) + (1 << 24)
+    assert wf["wf_queue_bytes"] <= wf["workspace_bytes"] < wf["device_free_bytes"]
+    srt = scene.plan(mcpt.RenderParams(pipeline="wavefront", wf_sort=True, **c2))
+    assert 3 * 160 * (1 << 27) <= srt["wf_queue_bytes"] < 3 * 161 * (1 << 27) + (1 << 24)
     mk = scene.plan(mcpt.RenderParams(**c2))
     assert mk["pipeline"] == 0 and mk["ready_thresh"] == 32 and mk["tail_units"] > 0 and mk["variant"] in (1, 2)
     o = scene.plan(mcpt.RenderParams(pipeline="wavefront", wf_streams=2, wf_refill=8, wf_batch=1 << 26, **c2))
@@ -229,3 +233,31 @@ def test_wavefront_render_captured_in_a_graph(mcpt):
         g.replay()
     torch.cuda.synchronize()
     assert np.array_equal(fb.view(96, 128, 4)[..., :3].cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("pipeline", ["megakernel", "wavefront"])
+def test_rccl_gather_one_device(mcpt, devices, pipeline):
+    """mcpt_render_params::gather = RCCL (capi.cpp render_multi: ncclCommInitAll
+    over mcpt_init's device list, one grouped ncclGather into devices[0]'s
+    gather buffer, the unpermute with the running mean) on a one-device list,
+    i.e. a one-rank communicator: the plain render's image bit for bit, for a
+    progressive second call too and through render_device after reserve.  A
+    list naming one GPU twice is refused by RCCL's communicator set-up
+    (scripts/rccl_probe.py); two distinct GPUs need the driver's node."""
+    import torch
+    devices([0])
+    scene = mcpt.Scene(mcpt.ObjModel(mcpt.scene_path("scene01")))
+    kw = dict(width=67, height=45, spp=5, spp_chunk=2, pipeline=pipeline)
+    ref0, st0 = scene.render(mcpt.RenderParams(**kw))
+    ref1, _ = scene.render(mcpt.RenderParams(spp_offset=5, prev_count=1, **kw), ref0.copy())
+    img0, st = scene.render(mcpt.RenderParams(gather="rccl", **kw))
+    assert np.array_equal(img0.view(np.uint32), ref0.view(np.uint32))
+    assert st["rays"] == st0["rays"]
+    img1, _ = scene.render(mcpt.RenderParams(gather="rccl", spp_offset=5, prev_count=1, **kw), img0.copy())
+    assert np.array_equal(img1.view(np.uint32), ref1.view(np.uint32))
+    p = mcpt.RenderParams(gather="rccl", **kw)
+    scene.reserve(p)
+    fb = torch.zeros((45 * 67, 4), dtype=torch.float32, device="cuda")
+    scene.render_device(p, fb.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(fb.view(45, 67, 4)[..., :3].cpu().numpy(), ref0)
