@@ -131,8 +131,19 @@ __device__ __forceinline__ void stq(float4* p, float4 v) {
 // a plain k -> k (an image of 2^14 8x8 tiles, 256 segments) each segment got
 // the same 64 tiles for every sample -- a fixed stripe of the image, whose
 // cost differs from the others' and left CUs idle at the end of every extend.
+// MCPT_WF_XCD: the rotation is a multiple of 8, so group k of every block goes
+// to a segment g = k (mod 8).  Extend and shade workgroup g (one per segment)
+// is dispatched to XCD g mod 8, and a group's image region (an 8x8 tile; a
+// 1024x16 strip of 2^14 paths for global-memory scenes) is k mod (regions per
+// sample): every sample of a region then runs on the same XCD, whose L2 holds
+// the part of the scene image that region's paths walk.
+#ifndef MCPT_WF_XCD
+#define MCPT_WF_XCD 1
+#endif
 __device__ __forceinline__ uint32_t seg_of(uint32_t k, uint32_t b, uint32_t nseg) {
-    const uint32_t rot = (uint32_t)(((uint64_t)(b * 2654435761u) * nseg) >> 32);
+    const uint32_t rot = (MCPT_WF_XCD && (nseg & 7u) == 0u)
+                             ? (uint32_t)(((uint64_t)(b * 2654435761u) * (nseg >> 3)) >> 32) << 3
+                             : (uint32_t)(((uint64_t)(b * 2654435761u) * nseg) >> 32);
     const uint32_t g = k + rot;
     return g >= nseg ? g - nseg : g;
 }

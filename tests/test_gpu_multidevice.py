@@ -191,6 +191,15 @@ def test_wavefront_memory_budget(mcpt):
     with pytest.raises(mcpt.McptError) as e:
         scene.render(mcpt.RenderParams(wf_mem_limit=1 << 20, wf_batch=1 << 20, **kw))
     assert e.value.code == -5 and "wavefront queues" in str(e.value)
+    # a reserved scene keeps its reservation: later default-batch renders are
+    # fitted into the reserved queue bytes (no re-allocation, e.g. inside a
+    # stream capture), with the same image
+    fresh = mcpt.Scene(mcpt.ObjModel(mcpt.scene_path("scene01")))
+    fresh.reserve(mcpt.RenderParams(wf_mem_limit=lim, **kw))
+    after = fresh.plan(mcpt.RenderParams(**kw))
+    assert after["wf_batch"] == small["wf_batch"] and after["wf_queue_bytes"] <= lim
+    img2, _ = fresh.render(mcpt.RenderParams(**kw))
+    assert np.array_equal(img2, ref)
 
 
 def test_global_layout_option_matches_oracle(mcpt, oracle_mod):
