@@ -27,6 +27,10 @@ inline mcpt_scene*& scene() {      // the reference keeps the scene in module gl
     static mcpt_scene* s = nullptr;
     return s;
 }
+inline int32_t& gather() {           // how a multi-device render's shards reach devices[0]
+    static int32_t g = MCPT_GATHER_PEER;
+    return g;
+}
 }  // namespace detail
 
 inline int Initialize() {            // CUTracer.cu:220-223: cudaSetDevice(0)
@@ -41,6 +45,11 @@ inline int Initialize() {            // CUTracer.cu:220-223: cudaSetDevice(0)
 inline int Initialize(const std::vector<int32_t>& devices) {
     return mcpt_init(devices.data(), static_cast<int32_t>(devices.size()));
 }
+
+// RenderScene's gather for such a device list: one RCCL collective over the
+// list (ncclCommInitAll + ncclGather into devices[0]) instead of peer copies
+// (mcpt_render_params::gather); also valid for a one-device list.
+inline void UseRcclGather(bool on) { detail::gather() = on ? MCPT_GATHER_RCCL : MCPT_GATHER_PEER; }
 
 // ObjModelT: PW::FileReader::ObjModel (ObjReader.hpp:37-63): m_vertices, m_normals
 // (x,y,z floats), m_triangles (m_vertexIndex[3], m_textureIndex[3], m_normalIndex[3],
@@ -118,6 +127,7 @@ int RenderScene(const int sceneID, Vec3T* hostcolor, int width = 800, int height
     p.height = height;
     p.spp = static_cast<uint32_t>(spp_per_kernel);
     p.spp_chunk = static_cast<uint32_t>(spp_chunk > 0 ? spp_chunk : 0);
+    p.gather = detail::gather();
     p.eye[2] = (sceneID == 1) ? 17.0f : 23.0f;
     for (int k = 0; k < num_kernels; ++k) {
         p.spp_offset = static_cast<uint32_t>(k * spp_per_kernel);

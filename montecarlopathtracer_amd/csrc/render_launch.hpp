@@ -29,7 +29,7 @@ namespace mcpt {
 // two-level groups and mark the group roots (bit 29 of an inner node word;
 // trace_device.hpp descend_steps, capi.cpp device_order_groups)
 #ifndef MCPT_KD_GROUPS
-#define MCPT_KD_GROUPS 1
+#define MCPT_KD_GROUPS 0
 #endif
 
 constexpr int kLdsBlock = 1024;          // in-LDS variant: one 16-wave workgroup per CU

@@ -68,6 +68,7 @@ int main(int argc, char** argv) {
         c = *end ? end + 1 : end;
     }
     const int init = devices.empty() ? PW::Tracer::Initialize() : PW::Tracer::Initialize(devices);
+    if (argc > 5 && std::string(argv[5]) == "rccl") PW::Tracer::UseRcclGather(true);
     if (init != 0 || PW::Tracer::CreateGeometry(&model) != 0 ||
         PW::Tracer::RenderScene(1, hostcolor.data(), W, H, 3, argc > 4 ? std::atoi(argv[4]) : 4) != 0) {
         std::printf("tracer: %s\n", mcpt_last_error());

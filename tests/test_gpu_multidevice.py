@@ -270,3 +270,22 @@ def test_rccl_gather_one_device(mcpt, devices, pipeline):
     scene.render_device(p, fb.data_ptr(), torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     assert np.array_equal(fb.view(45, 67, 4)[..., :3].cpu().numpy(), ref0)
+
+
+def test_pw_tracer_dropin_rccl_gather(mcpt, tmp_path):
+    """The C++ drop-in (include/mcpt_pw_tracer.hpp) reaching RCCL: Initialize({0})
+    + UseRcclGather(true), then the reference's RenderScene loop -- every launch
+    a one-rank ncclGather through the C ABI -- renders the Python mirror's image."""
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "cpp"))
+    import build_dropin
+    exe = build_dropin.build()
+    out = str(tmp_path / "img.bin")
+    r = subprocess.run([exe, mcpt.scene_path("scene01"), out, "0", "4", "rccl"], capture_output=True, text=True)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+    got = np.fromfile(out, np.float32).reshape(30, 40, 3)
+    tr = mcpt.Tracer()
+    tr.initialize([0])
+    tr.create_geometry(mcpt.ObjModel(mcpt.scene_path("scene01")))
+    host = np.zeros((30, 40, 3), np.float32)
+    tr.render_scene(1, host, num_kernels=3, samples_per_kernel=4)
+    assert np.array_equal(got, host)
