@@ -176,6 +176,7 @@ struct WfParams {
     int32_t bounce;
     int32_t refill_thresh;               // idle lanes before an extend wave refills
     int32_t sort;                        // 1: material sort (class lists), 0: shade in queue order
+    uint32_t xcd_deal;                   // 1: groups dealt to segments by XCD (global-memory scenes, seg_of)
 };
 
 size_t lds_bytes_in_lds(uint32_t image_bytes, int S);

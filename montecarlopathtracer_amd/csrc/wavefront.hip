@@ -131,17 +131,21 @@ __device__ __forceinline__ void stq(float4* p, float4 v) {
 // a plain k -> k (an image of 2^14 8x8 tiles, 256 segments) each segment got
 // the same 64 tiles for every sample -- a fixed stripe of the image, whose
 // cost differs from the others' and left CUs idle at the end of every extend.
-// MCPT_WF_XCD: the rotation is a multiple of 8, so group k of every block goes
-// to a segment g = k (mod 8).  Extend and shade workgroup g (one per segment)
-// is dispatched to XCD g mod 8, and a group's image region (an 8x8 tile; a
-// 1024x16 strip of 2^14 paths for global-memory scenes) is k mod (regions per
-// sample): every sample of a region then runs on the same XCD, whose L2 holds
-// the part of the scene image that region's paths walk.
+// WfParams::xcd_deal (global-memory scenes, MCPT_WF_XCD): the rotation is a
+// multiple of 8, so group k of every block goes to a segment g = k (mod 8).
+// Extend and shade workgroup g (one per segment) is dispatched to XCD g mod 8,
+// and a group's image region (a 1024x16 strip of 2^14 paths) is k mod (regions
+// per sample): every sample of a region then runs on the same XCD, whose L2
+// and the caches behind it serve the part of the scene image that region's
+// paths walk.  C4 +1.6% (9.31 / 9.34 -> 9.48 / 9.48 G rays/s; serialized
+// extends 880 -> 771 ms per two frames at the same L2 hit rate, 0.776 /
+// 0.778); LDS scenes keep the finer rotation (C2 -2.3% with it: the coarser
+// rotation balances the segments' work less well).
 #ifndef MCPT_WF_XCD
 #define MCPT_WF_XCD 1
 #endif
-__device__ __forceinline__ uint32_t seg_of(uint32_t k, uint32_t b, uint32_t nseg) {
-    const uint32_t rot = (MCPT_WF_XCD && (nseg & 7u) == 0u)
+__device__ __forceinline__ uint32_t seg_of(uint32_t k, uint32_t b, uint32_t nseg, bool xcd) {
+    const uint32_t rot = (MCPT_WF_XCD && xcd && (nseg & 7u) == 0u)
                              ? (uint32_t)(((uint64_t)(b * 2654435761u) * (nseg >> 3)) >> 32) << 3
                              : (uint32_t)(((uint64_t)(b * 2654435761u) * nseg) >> 32);
     const uint32_t g = k + rot;
@@ -151,7 +155,7 @@ __device__ __forceinline__ uint32_t seg_of(uint32_t k, uint32_t b, uint32_t nseg
 // Inverse of generate's dealing: path id of local slot j of segment g's queue 0.
 __device__ __forceinline__ uint32_t slot_pid(const WfParams& wf, uint32_t g, uint32_t j) {
     const uint32_t gs = wf.group_shift, blk = j >> gs;
-    const uint32_t rot = seg_of(0, blk, wf.nseg);
+    const uint32_t rot = seg_of(0, blk, wf.nseg, wf.xcd_deal);
     const uint32_t k = g >= rot ? g - rot : g + wf.nseg - rot;
     return ((blk * wf.nseg + k) << gs) | (j & ((1u << gs) - 1u));
 }
@@ -165,10 +169,10 @@ __device__ __forceinline__ uint32_t seg_queue0_len(const WfParams& wf, uint32_t 
     const uint32_t ngroups = (n + gm) >> gs;
     const uint32_t full = ngroups / wf.nseg, rem = ngroups - full * wf.nseg;
     // block `full` (partial, rem groups) covers segments rot, rot+1, ... (mod nseg)
-    const uint32_t k = (g + wf.nseg - seg_of(0, full, wf.nseg)) % wf.nseg;
+    const uint32_t k = (g + wf.nseg - seg_of(0, full, wf.nseg, wf.xcd_deal)) % wf.nseg;
     uint32_t len = (full + (k < rem ? 1u : 0u)) << gs;
     const uint32_t lb = (ngroups - 1u) / wf.nseg;            // block of the last group
-    if (seg_of(ngroups - 1u - lb * wf.nseg, lb, wf.nseg) == g) len -= (ngroups << gs) - n;
+    if (seg_of(ngroups - 1u - lb * wf.nseg, lb, wf.nseg, wf.xcd_deal) == g) len -= (ngroups << gs) - n;
     return len;
 }
 
@@ -210,7 +214,7 @@ __global__ void __launch_bounds__(kGenBlock) wf_generate(const KernelParams kp, 
         const uint32_t s_local = pid / wf.nb;
         const uint32_t v = wf.v0 + (pid - s_local * wf.nb);
         const uint32_t grp = pid >> gs, blk = grp / wf.nseg;
-        const uint32_t g = seg_of(grp - blk * wf.nseg, blk, wf.nseg);
+        const uint32_t g = seg_of(grp - blk * wf.nseg, blk, wf.nseg, wf.xcd_deal);
         const uint32_t slot = g * wf.seg + (blk << gs) + (pid & gm);
         if (grp < wf.nseg && (pid & gm) == 0u) wf.cnt[g].queued = seg_queue0_len(wf, g);   // segment g's queue length
         int px, py;
@@ -1078,6 +1082,7 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams* wf_in, co
             // LDS scenes: one 8x8 tile of one sample per group; global-memory
             // scenes: the planned group size (whole image regions per segment)
             wf.group_shift = in_lds ? 6u : wf_in[h].group_shift;
+            wf.xcd_deal = in_lds ? 0u : 1u;                                // (seg_of)
             // whole groups per segment
             wf.seg = ((((n + (1u << wf.group_shift) - 1u) >> wf.group_shift) + nseg - 1) / nseg) << wf.group_shift;
             e = hipMemsetAsync(wf.cnt, 0, sizeof(WfCounters) * (size_t)nseg * (size_t)(max_bounces + 1), bs);
