@@ -303,6 +303,12 @@ struct ClassBuf {
 #endif
 constexpr int kWfLdsCap = MCPT_KD_GROUPS ? MCPT_WF_GROUP_CAP : MCPT_WF_DESCENT_CAP;
 
+// LDS stack entries per lane of the global-memory extend (256-thread
+// workgroups, kGlobalBlocksPerCu per CU per launch; a smaller stack lets other
+// streams' extend workgroups share the CU)
+#ifndef MCPT_WF_GLOBAL_S
+#define MCPT_WF_GLOBAL_S 8
+#endif
 #ifndef MCPT_WF_GEO_LDS
 #define MCPT_WF_GEO_LDS 1
 #endif
@@ -1076,7 +1082,7 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams* wf_in, co
             // the shade's material table in LDS if it fits beside the extend's
             // workgroups on a CU (MCPT_WF_GEO_LDS)
             const size_t ext_lds = in_lds ? lds_bytes_in_lds(img, 4) + 32
-                                          : (size_t)kGlobalBlocksPerCu * (8 * kGlobalBlock * 16 + 32);
+                                          : (size_t)kGlobalBlocksPerCu * (MCPT_WF_GLOBAL_S * kGlobalBlock * 16 + 32);
             const size_t geo_bytes = (MCPT_WF_GEO_LDS && ext_lds + 64 * (size_t)kp.scene.n_geoms + 64 <= kLdsPerCu)
                                          ? 64 * (size_t)kp.scene.n_geoms : 0;
             // LDS scenes: one 8x8 tile of one sample per group; global-memory
@@ -1106,7 +1112,8 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams* wf_in, co
                 else if (in_lds)
                     e = launch_extend<true, 4, kLdsBlock>(kb, wf, (int)nseg, lds_bytes_in_lds(img, 4) + 32, bs);
                 else
-                    e = launch_extend<false, 8, kGlobalBlock>(kb, wf, (int)nseg, (size_t)8 * kGlobalBlock * 16 + 32,
+                    e = launch_extend<false, MCPT_WF_GLOBAL_S, kGlobalBlock>(kb, wf, (int)nseg,
+                                                                            (size_t)MCPT_WF_GLOBAL_S * kGlobalBlock * 16 + 32,
                                                               bs);
                 if (e != hipSuccess) break;
                 if (wf.sort)
