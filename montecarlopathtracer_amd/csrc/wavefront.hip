@@ -304,10 +304,13 @@ struct ClassBuf {
 constexpr int kWfLdsCap = MCPT_KD_GROUPS ? MCPT_WF_GROUP_CAP : MCPT_WF_DESCENT_CAP;
 
 // LDS stack entries per lane of the global-memory extend (256-thread
-// workgroups, kGlobalBlocksPerCu per CU per launch; a smaller stack lets other
-// streams' extend workgroups share the CU)
+// workgroups, kGlobalBlocksPerCu per CU per launch).  6 (24 KB per workgroup):
+// a fifth extend workgroup -- another stream's -- fits on a CU beside four
+// (5 x 88 VGPRs + a 64-VGPR shade wave per SIMD) and the stack still rarely
+// spills: C4 9.46 / 9.47 -> 9.61 / 9.63 G rays/s (+1.6%); 8 entries (32 KB,
+// four workgroups) was the round-3 default, 4 entries spill too often (8.78 / 8.80)
 #ifndef MCPT_WF_GLOBAL_S
-#define MCPT_WF_GLOBAL_S 8
+#define MCPT_WF_GLOBAL_S 6
 #endif
 #ifndef MCPT_WF_GEO_LDS
 #define MCPT_WF_GEO_LDS 1
