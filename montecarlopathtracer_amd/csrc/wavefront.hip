@@ -304,13 +304,15 @@ struct ClassBuf {
 constexpr int kWfLdsCap = MCPT_KD_GROUPS ? MCPT_WF_GROUP_CAP : MCPT_WF_DESCENT_CAP;
 
 // LDS stack entries per lane of the global-memory extend (256-thread
-// workgroups, kGlobalBlocksPerCu per CU per launch).  6 (24 KB per workgroup):
+// workgroups, kGlobalBlocksPerCu per CU per launch).  7 (28 KB per workgroup):
 // a fifth extend workgroup -- another stream's -- fits on a CU beside four
-// (5 x 88 VGPRs + a 64-VGPR shade wave per SIMD) and the stack still rarely
-// spills: C4 9.46 / 9.47 -> 9.61 / 9.63 G rays/s (+1.6%); 8 entries (32 KB,
-// four workgroups) was the round-3 default, 4 entries spill too often (8.78 / 8.80)
+// (5 x 88 VGPRs + a 64-VGPR shade wave per SIMD; 5 x 28 KB + the shade's table
+// of LDS) and the stack still rarely spills.  C4 G rays/s, two boxes: S = 8
+// (32 KB, four workgroups per CU, the round-3 default) 9.46 / 9.47, S = 6
+// 9.61 / 9.63 and 9.65 / 9.59, S = 7 9.85 / 9.87, S = 5 9.20 / 9.18, S = 4
+// 8.78 / 8.80 (spills)
 #ifndef MCPT_WF_GLOBAL_S
-#define MCPT_WF_GLOBAL_S 6
+#define MCPT_WF_GLOBAL_S 7
 #endif
 #ifndef MCPT_WF_GEO_LDS
 #define MCPT_WF_GEO_LDS 1
