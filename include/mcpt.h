@@ -111,7 +111,7 @@ typedef struct {
     int32_t wf_refill;          /* wavefront extend: ready lanes before a wave refills (1..64);
                                    0: 16 (LDS scenes), 8 (global-memory scenes) */
     int32_t wf_group_shift;     /* wavefront, global-memory scenes: paths are dealt to queue
-                                   segments in groups of 2^k (6..14); 0: 14 */
+                                   segments in groups of 2^k (6..14); 0: 12 */
     int32_t ready_thresh;       /* megakernel: ready lanes before a shading round (1..64);
                                    0: 32 (LDS scenes), 40 (global-memory scenes) */
     int32_t tail_units_per_lane;/* megakernel tail split: the last units per lane handed out one

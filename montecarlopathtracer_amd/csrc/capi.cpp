@@ -637,9 +637,11 @@ Plan make_plan(const mcpt_scene& s, const mcpt_render_params* p) {
     // 8 / 16 / 24: 10.08 / 10.28 / 10.19 G rays/s), 8 for scenes in global
     // memory (C4 256 spp, 2..40: 6.18 / 6.20 (4-12) / 6.14 (16) / 5.79 (32) / 5.53)
     pl.wf_refill = p->wf_refill > 0 ? p->wf_refill : (s.gpu.node_boxes ? 8 : 16);
-    // global-memory scenes keep whole image regions together per segment (C4
-    // sweep: 2^6 0.63, 2^8 0.47, 2^10 0.44, 2^12 0.62, contiguous 0.79 G rays/s)
-    pl.wf_group_shift = s.gpu.node_boxes ? static_cast<uint32_t>(p->wf_group_shift > 0 ? p->wf_group_shift : 14) : 6u;
+    // global-memory scenes keep whole image regions together per segment.
+    // Round 4 (XCD-aware dealing, 7-entry stacks; C4 1024 spp, G rays/s):
+    // 2^8 9.36, 2^9 8.39, 2^10 7.92 / 7.86, 2^11 9.70 / 9.73, 2^12 9.96 / 9.96 /
+    // 9.98, 2^13 9.74, 2^14 9.83 / 9.87 / 9.85 (round 1, 256 spp: 2^14 best)
+    pl.wf_group_shift = s.gpu.node_boxes ? static_cast<uint32_t>(p->wf_group_shift > 0 ? p->wf_group_shift : 12) : 6u;
     // tail split: 4 units per lane (a whole frame +0.3% over 6; rank 0 of 8
     // shards at 97.0% of ideal, 6: 96.5%, 8: 95.7%, 10: 94.8%)
     pl.tail_per_lane = p->tail_units_per_lane == 0 ? 4 : p->tail_units_per_lane;
