@@ -303,16 +303,23 @@ struct ClassBuf {
 #endif
 constexpr int kWfLdsCap = MCPT_KD_GROUPS ? MCPT_WF_GROUP_CAP : MCPT_WF_DESCENT_CAP;
 
-// LDS stack entries per lane of the global-memory extend (256-thread
-// workgroups, kGlobalBlocksPerCu per CU per launch).  7 (28 KB per workgroup):
-// a fifth extend workgroup -- another stream's -- fits on a CU beside four
-// (5 x 88 VGPRs + a 64-VGPR shade wave per SIMD; 5 x 28 KB + the shade's table
-// of LDS) and the stack still rarely spills.  C4 G rays/s, two boxes: S = 8
-// (32 KB, four workgroups per CU, the round-3 default) 9.46 / 9.47, S = 6
-// 9.61 / 9.63 and 9.65 / 9.59, S = 7 9.85 / 9.87, S = 5 9.20 / 9.18, S = 4
-// 8.78 / 8.80 (spills)
+// Residency of the global-memory extend (C4: a walk bound by the latency of
+// node and triangle reads from L2 / MALL, so every resident wave counts).
+// Workgroups of 256 threads, kGlobalBlocksPerCu per CU per launch; other
+// streams' extends fill further slots as far as LDS and VGPRs allow.
+// MCPT_WF_GLOBAL_S: LDS stack entries per lane; MCPT_WF_GLOBAL_MINWG: resident
+// workgroups per CU the compiler must allow (its VGPR budget; the lean
+// queue-order kernel only -- the untimed counting kernels and the material
+// sort's class buffers keep their registers).  6 x 6: 80 VGPRs
+// (no scratch) and 6 x 24 KB of LDS, six extend waves per SIMD.  C4 G rays/s:
+// S = 8, no hint (round 3: 32 KB, four workgroups, 88 VGPRs) 9.46 / 9.47;
+// S = 6 9.61 / 9.63; S = 7 (five workgroups) 9.85 / 9.87; S = 5 9.20; S = 4
+// 8.78 (spills); S = 6 with six workgroups (80 VGPRs) 10.36 / 10.31.
 #ifndef MCPT_WF_GLOBAL_S
-#define MCPT_WF_GLOBAL_S 7
+#define MCPT_WF_GLOBAL_S 6
+#endif
+#ifndef MCPT_WF_GLOBAL_MINWG
+#define MCPT_WF_GLOBAL_MINWG 6
 #endif
 #ifndef MCPT_WF_GEO_LDS
 #define MCPT_WF_GEO_LDS 1
@@ -325,7 +332,8 @@ constexpr size_t kLdsPerCu = 160 * 1024;
 // carries no class-list buffers (8 VGPRs: the co-resident shade of the
 // multi-stream pipeline needs the extend at <= 96)
 template <bool IN_LDS, int S, int BLOCK, bool COUNT, bool SORT>
-__global__ void __launch_bounds__(BLOCK) wf_extend(const KernelParams kp, const WfParams wf) {
+__global__ void __launch_bounds__(BLOCK, (!IN_LDS && !COUNT && !SORT && MCPT_WF_GLOBAL_MINWG) ? MCPT_WF_GLOBAL_MINWG : 1)
+wf_extend(const KernelParams kp, const WfParams wf) {
     static_assert((BLOCK & (BLOCK - 1)) == 0, "stack slot addresses (slot_of) mask by a power-of-two block");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t g = blockIdx.x;
