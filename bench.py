@@ -57,7 +57,7 @@ def algorithmic_bytes(st: dict, pixels: int) -> dict:
 def _workload_args(args, shard=(1, 0)) -> list:
     return ["--scene", args.scene, "--width", str(args.width), "--height", str(args.height), "--spp", str(args.spp),
             "--spp-chunk", str(args.spp_chunk), "--pipeline", args.pipeline, "--wf-batch", str(args.wf_batch),
-            "--wf-streams", str(args.wf_streams), "--pmc-shard", f"{shard[0]},{shard[1]}"] + \
+            "--wf-streams", str(args.wf_streams), "--pmc-shard", f"{shard[0]},{shard[1]}", "--layout", args.layout] + \
         [x for kv in args.set for x in ("--set", kv)] + (["--counting"] if args.counting else [])
 
 
@@ -370,6 +370,9 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--scene", default="scene01")
+    ap.add_argument("--layout", choices=["auto", "global"], default="auto",
+                    help="scene image placement (mcpt_scene_options::layout): LDS when it fits, or global memory "
+                         "with child-box records")
     ap.add_argument("--width", type=int, default=1024)
     ap.add_argument("--height", type=int, default=1024)
     ap.add_argument("--spp", type=int, default=1024)
@@ -440,7 +443,7 @@ def main():
     M.Tracer().initialize(devices if n_dev > 1 else [dev.index])
     n_gpus = world * n_dev
 
-    scene = M.Scene(M.ObjModel(M.scene_path(args.scene)))
+    scene = M.Scene(M.ObjModel(M.scene_path(args.scene)), layout=args.layout)
     scene_id = 2 if args.scene in ("scene02", "scene03") else 1
     if args.pmc_child:   # PMC pass: exactly one render of the timed kernel (rank 0's shard), then exit
         sc, si = (int(x) for x in args.pmc_shard.split(","))

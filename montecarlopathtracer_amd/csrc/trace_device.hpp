@@ -298,6 +298,9 @@ __device__ __forceinline__ float4 ld_tri(const float4* __restrict__ p) {
 #ifndef MCPT_DESCENT_CAP_GLOBAL
 #define MCPT_DESCENT_CAP_GLOBAL 5                // global-memory scenes (C4: 5 > 4)
 #endif
+#ifndef MCPT_REC_TAIL8
+#define MCPT_REC_TAIL8 0                         // 1: the pair record's third load is 8 B (global scenes)
+#endif
 #ifndef MCPT_GROUP_LOAD
 #define MCPT_GROUP_LOAD 0                        // 1: a node group's child pairs read by roots only
 #endif
@@ -515,7 +518,14 @@ __device__ __forceinline__ int descend_steps(RayState& r, const uint2* __restric
             const uint4* rec = pairs + 3u * ((left - 1u) >> 1);
             pr = rec[0];
             bx0 = rec[1];
+#if MCPT_REC_TAIL8
+            {   // the record's last 8 B are padding: an 8-B load for the right box's tail
+                const uint2 t = *reinterpret_cast<const uint2*>(rec + 2);
+                bx1 = make_uint4(t.x, t.y, 0u, 0u);
+            }
+#else
             bx1 = rec[2];
+#endif
         } else {
             pr = *reinterpret_cast<const uint4*>(nodes1 + left);   // children left, left+1
         }
