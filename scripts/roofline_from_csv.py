@@ -36,7 +36,7 @@ def main(d, line=None, cus=256):
             v = b.read_wf_kernels(vd)["extend"]
             roof["valu"] = b.valu_block(v, cus, v["ns"] / 1e6, ln["rays_per_step"] / ln["n_gpus"])
         ldd = os.path.join(d, "wf_lds")
-        if os.path.isdir(ldd):
+        if os.path.isdir(ldd) and ln["config"].get("kernel_variant") == 4:   # scene image in LDS
             lc = b.read_wf_kernels(ldd)["extend"]
             pr = r["algorithmic"]["per_ray"]
             rays = ln["rays_per_step"] / ln["n_gpus"]
