@@ -73,9 +73,10 @@ __device__ __forceinline__ lds_uint4* slot_of(uint4* st, int stride, int32_t pos
     // address 0 and a lane's base is below one slot row): one v_and_or_b32
     const uint32_t base = (uint32_t)(size_t)(lds_uint4*)st;
     const uint32_t row = (uint32_t)stride * 16u;
-    if constexpr ((S & (S - 1)) == 0) {
+    // (stride is a compile-time block size after inlining, so the test folds)
+    if (((S & (S - 1)) == 0) && ((stride & (stride - 1)) == 0)) {
         return (lds_uint4*)(size_t)(((uint32_t)pos & ((uint32_t)(S - 1) * row)) | base);
-    } else {                                  // (a stack of S != 2^k entries: the row index mod S)
+    } else {                                  // (S or the block not 2^k: the row index mod S)
         return (lds_uint4*)(size_t)(((uint32_t)pos / row % (uint32_t)S) * row + base);
     }
 }

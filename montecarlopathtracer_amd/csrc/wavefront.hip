@@ -325,16 +325,24 @@ constexpr int kWfLdsCap = MCPT_KD_GROUPS ? MCPT_WF_GROUP_CAP : MCPT_WF_DESCENT_C
 #define MCPT_WF_GEO_LDS 1
 #endif
 constexpr size_t kLdsPerCu = 160 * 1024;
+constexpr int kLayGlobal = 0, kLayLds = 1, kLayHybrid = 2;
+
 
 // ---- extend: closest hit of every ray of this workgroup's segment -----------
 // COUNT = false (lean renders): the traversal counters are compiled out.
 // SORT = WfParams::sort, a template argument so that the queue-order variant
 // carries no class-list buffers (8 VGPRs: the co-resident shade of the
 // multi-stream pipeline needs the extend at <= 96)
-template <bool IN_LDS, int S, int BLOCK, bool COUNT, bool SORT>
-__global__ void __launch_bounds__(BLOCK, (!IN_LDS && !COUNT && !SORT && MCPT_WF_GLOBAL_MINWG) ? MCPT_WF_GLOBAL_MINWG : 1)
+// LAY: kLayGlobal (scene image with child-box records in global memory),
+// kLayLds (the whole 8-B-node image copied into LDS), kLayHybrid (node words,
+// leaf refs and geometries in LDS, triangle records read through L1/L2:
+// MCPT_WF_HYBRID, two workgroups per CU)
+template <int LAY, int S, int BLOCK, bool COUNT, bool SORT>
+__global__ void __launch_bounds__(BLOCK, (LAY == kLayGlobal && !COUNT && !SORT && MCPT_WF_GLOBAL_MINWG)
+                                             ? MCPT_WF_GLOBAL_MINWG
+                                             : (LAY == kLayHybrid ? 6 : 1))   // (waves per SIMD)
 wf_extend(const KernelParams kp, const WfParams wf) {
-    static_assert((BLOCK & (BLOCK - 1)) == 0, "stack slot addresses (slot_of) mask by a power-of-two block");
+    constexpr bool IN_LDS = LAY != kLayGlobal;            // node words in LDS
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t g = blockIdx.x;
     WfCounters* cn = wf.cnt + (size_t)wf.bounce * wf.nseg + g;
@@ -345,23 +353,26 @@ wf_extend(const KernelParams kp, const WfParams wf) {
     }
     const int tid = (int)threadIdx.x;
     const GpuScene& sc = kp.scene;
-    // LDS: [stack S x BLOCK x 16 B | scene image (IN_LDS) | 5 counters]
+    // LDS: [stack S x BLOCK x 16 B | scene image (kLayLds) or its part from the
+    // nodes on (kLayHybrid) | 5 counters]
     unsigned char* const lds_image = smem + (size_t)S * BLOCK * 16;
-    uint32_t* lcnt = reinterpret_cast<uint32_t*>(lds_image + (IN_LDS ? sc.image_bytes : 0u));
+    const uint32_t lds_from = LAY == kLayHybrid ? sc.off_nodes : 0u;   // image offset of lds_image[0]
+    uint32_t* lcnt = reinterpret_cast<uint32_t*>(lds_image + (IN_LDS ? sc.image_bytes - lds_from : 0u));
     if (tid < 5) lcnt[tid] = 0;
     const float4* tris;
     const uint2* nodes;
     const uint32_t* leafs;
     const GpuGeom* geoms;
     if constexpr (IN_LDS) {
-        const uint4* src = reinterpret_cast<const uint4*>(sc.image);
+        const uint4* src = reinterpret_cast<const uint4*>(sc.image + lds_from);
         uint4* dst = reinterpret_cast<uint4*>(lds_image);
-        const uint32_t n16 = sc.image_bytes / 16u;
+        const uint32_t n16 = (sc.image_bytes - lds_from) / 16u;
         for (uint32_t i = (uint32_t)tid; i < n16; i += BLOCK) dst[i] = src[i];
-        tris = reinterpret_cast<const float4*>(lds_image + sc.off_tris);
-        nodes = reinterpret_cast<const uint2*>(lds_image + sc.off_nodes) + 1;
-        leafs = reinterpret_cast<const uint32_t*>(lds_image + sc.off_leafs);
-        geoms = reinterpret_cast<const GpuGeom*>(lds_image + sc.off_geoms);
+        tris = LAY == kLayLds ? reinterpret_cast<const float4*>(lds_image + sc.off_tris)
+                              : reinterpret_cast<const float4*>(sc.image + sc.off_tris);
+        nodes = reinterpret_cast<const uint2*>(lds_image + (sc.off_nodes - lds_from)) + 1;
+        leafs = reinterpret_cast<const uint32_t*>(lds_image + (sc.off_leafs - lds_from));
+        geoms = reinterpret_cast<const GpuGeom*>(lds_image + (sc.off_geoms - lds_from));
     } else {
         tris = reinterpret_cast<const float4*>(sc.image + sc.off_tris);
         nodes = reinterpret_cast<const uint2*>(sc.image + sc.off_nodes) + 1;
@@ -432,7 +443,7 @@ wf_extend(const KernelParams kp, const WfParams wf) {
             }
 #endif
             if (mode == kTrav) {
-                if (trav_iter<S, !IN_LDS, COUNT, IN_LDS, IN_LDS ? kWfLdsCap : MCPT_WF_DESCENT_CAP_GLOBAL>(r, tris, nodes, leafs, st, BLOCK, spill, spill_stride, c MCPT_LU_ARG,
+                if (trav_iter<S, !IN_LDS, COUNT, LAY == kLayLds, IN_LDS ? kWfLdsCap : MCPT_WF_DESCENT_CAP_GLOBAL>(r, tris, nodes, leafs, st, BLOCK, spill, spill_stride, c MCPT_LU_ARG,
                                                  pairs))
                     mode = kReady;
             }
@@ -550,9 +561,10 @@ __device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin
 #ifndef MCPT_WF_GEN0
 #define MCPT_WF_GEN0 1
 #endif
-template <int S, int BLOCK, bool COUNT>
-__global__ void __launch_bounds__(BLOCK) wf_extend_primary(const KernelParams kp, const WfParams wf) {
-    static_assert((BLOCK & (BLOCK - 1)) == 0, "stack slot addresses (slot_of) mask by a power-of-two block");
+template <int LAY, int S, int BLOCK, bool COUNT>
+__global__ void __launch_bounds__(BLOCK, LAY == kLayHybrid ? 6 : 1) wf_extend_primary(const KernelParams kp,
+                                                                                 const WfParams wf) {
+    static_assert(LAY != kLayGlobal, "the packet walk reads node words from LDS");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t g = blockIdx.x;
     WfCounters* cn = wf.cnt + (size_t)wf.bounce * wf.nseg + g;
@@ -572,19 +584,21 @@ __global__ void __launch_bounds__(BLOCK) wf_extend_primary(const KernelParams kp
     const int tid = (int)threadIdx.x;
     const int lane = tid & 63;
     const GpuScene& sc = kp.scene;
-    // LDS: [stack S x BLOCK x 16 B | scene image | group counter]
+    // LDS: [stack S x BLOCK x 16 B | scene image (from the nodes on: kLayHybrid) | group counter]
     unsigned char* const lds_image = smem + (size_t)S * BLOCK * 16;
-    uint32_t* lgrp = reinterpret_cast<uint32_t*>(lds_image + sc.image_bytes);
+    const uint32_t lds_from = LAY == kLayHybrid ? sc.off_nodes : 0u;
+    uint32_t* lgrp = reinterpret_cast<uint32_t*>(lds_image + (sc.image_bytes - lds_from));
     if (tid == 0) *lgrp = 0;
     {
-        const uint4* src = reinterpret_cast<const uint4*>(sc.image);
+        const uint4* src = reinterpret_cast<const uint4*>(sc.image + lds_from);
         uint4* dst = reinterpret_cast<uint4*>(lds_image);
-        const uint32_t n16 = sc.image_bytes / 16u;
+        const uint32_t n16 = (sc.image_bytes - lds_from) / 16u;
         for (uint32_t i = (uint32_t)tid; i < n16; i += BLOCK) dst[i] = src[i];
     }
-    const float4* tris = reinterpret_cast<const float4*>(lds_image + sc.off_tris);
-    const uint2* nodes = reinterpret_cast<const uint2*>(lds_image + sc.off_nodes) + 1;
-    const uint32_t* leafs = reinterpret_cast<const uint32_t*>(lds_image + sc.off_leafs);
+    const float4* tris = LAY == kLayLds ? reinterpret_cast<const float4*>(lds_image + sc.off_tris)
+                                        : reinterpret_cast<const float4*>(sc.image + sc.off_tris);
+    const uint2* nodes = reinterpret_cast<const uint2*>(lds_image + (sc.off_nodes - lds_from)) + 1;
+    const uint32_t* leafs = reinterpret_cast<const uint32_t*>(lds_image + (sc.off_leafs - lds_from));
     __syncthreads();
     uint4* st = reinterpret_cast<uint4*>(smem) + tid;
     uint4* spill = kp.spill + (blockIdx.x * BLOCK + (uint32_t)tid);
@@ -721,9 +735,10 @@ __global__ void __launch_bounds__(BLOCK) wf_extend_primary(const KernelParams kp
                         const bool two = lend - i >= 2u;
                         const uint32_t k0 = leafs[i], k1n = leafs[i + 1u];
                         const uint32_t k1 = two ? k1n : k0;
-                        const float4 a0 = ld_tri<true>(tris + k0), a1 = ld_tri<true>(tris + k0 + 1);
-                        const float4 a2 = ld_tri<true>(tris + k0 + 2), b0 = ld_tri<true>(tris + k1);
-                        const float4 b1 = ld_tri<true>(tris + k1 + 1), b2 = ld_tri<true>(tris + k1 + 2);
+                        constexpr bool TL = LAY == kLayLds;
+                        const float4 a0 = ld_tri<TL>(tris + k0), a1 = ld_tri<TL>(tris + k0 + 1);
+                        const float4 a2 = ld_tri<TL>(tris + k0 + 2), b0 = ld_tri<TL>(tris + k1);
+                        const float4 b1 = ld_tri<TL>(tris + k1 + 1), b2 = ld_tri<TL>(tris + k1 + 2);
                         if (active) {
                             test_tri_pair(r, a0, a1, a2, k0, b0, b1, b2, k1, two);
                             if constexpr (COUNT) {
@@ -993,9 +1008,9 @@ __global__ void __launch_bounds__(256) wf_accumulate(const KernelParams kp, cons
 }
 
 
-template <int S, int BLOCK>
+template <int LAY, int S, int BLOCK>
 hipError_t launch_extend_primary(const KernelParams& kp, const WfParams& wf, int grid, size_t lds, hipStream_t st) {
-    auto kern = kp.lean ? wf_extend_primary<S, BLOCK, false> : wf_extend_primary<S, BLOCK, true>;
+    auto kern = kp.lean ? wf_extend_primary<LAY, S, BLOCK, false> : wf_extend_primary<LAY, S, BLOCK, true>;
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
@@ -1006,11 +1021,11 @@ hipError_t launch_extend_primary(const KernelParams& kp, const WfParams& wf, int
 template <int BLOCK>
 auto shade_kernel(bool geo_lds) { return geo_lds ? wf_shade_slots<BLOCK, true> : wf_shade_slots<BLOCK, false>; }
 
-template <bool IN_LDS, int S, int BLOCK>
+template <int LAY, int S, int BLOCK>
 hipError_t launch_extend(const KernelParams& kp, const WfParams& wf, int grid, size_t lds, hipStream_t st) {
-    auto kern = wf.sort ? (kp.lean ? wf_extend<IN_LDS, S, BLOCK, false, true> : wf_extend<IN_LDS, S, BLOCK, true, true>)
-                        : (kp.lean ? wf_extend<IN_LDS, S, BLOCK, false, false>
-                                   : wf_extend<IN_LDS, S, BLOCK, true, false>);
+    auto kern = wf.sort ? (kp.lean ? wf_extend<LAY, S, BLOCK, false, true> : wf_extend<LAY, S, BLOCK, true, true>)
+                        : (kp.lean ? wf_extend<LAY, S, BLOCK, false, false>
+                                   : wf_extend<LAY, S, BLOCK, true, false>);
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
@@ -1032,7 +1047,14 @@ void read_lane_use_wf(unsigned long long out[6]) {   // wavefront extend lane-us
 }
 #endif
 
-int wavefront_segments(const GpuScene& sc, int cus) { return wf_in_lds(sc) ? cus : cus * kGlobalBlocksPerCu; }
+int wavefront_segments(const GpuScene& sc, int cus) {
+    return wf_in_lds(sc) ? (MCPT_WF_HYBRID ? kHybridPerCu * cus : cus) : cus * kGlobalBlocksPerCu;
+}
+// LDS bytes of an LDS-scene extend workgroup: stack + image (or its part from the nodes on) + counters
+size_t wf_lds_extend_bytes(const GpuScene& sc) {
+    return MCPT_WF_HYBRID ? (size_t)kHybridS * kHybridBlock * 16 + (sc.image_bytes - sc.off_nodes) + 32
+                          : lds_bytes_in_lds(sc.image_bytes, 4) + 32;
+}
 
 hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams* wf_in, const WfStreams& ws, int cus,
                             int max_bounces, hipEvent_t ev0, hipEvent_t ev1, hipEvent_t ev2, float4* fb,
@@ -1094,7 +1116,7 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams* wf_in, co
             const uint32_t n = wf.nb * wf.ns;
             // the shade's material table in LDS if it fits beside the extend's
             // workgroups on a CU (MCPT_WF_GEO_LDS)
-            const size_t ext_lds = in_lds ? lds_bytes_in_lds(img, 4) + 32
+            const size_t ext_lds = in_lds ? (MCPT_WF_HYBRID ? kHybridPerCu : 1) * wf_lds_extend_bytes(kp.scene)
                                           : (size_t)kGlobalBlocksPerCu * (MCPT_WF_GLOBAL_S * kGlobalBlock * 16 + 32);
             const size_t geo_bytes = (MCPT_WF_GEO_LDS && ext_lds + 64 * (size_t)kp.scene.n_geoms + 64 <= kLdsPerCu)
                                          ? 64 * (size_t)kp.scene.n_geoms : 0;
@@ -1120,12 +1142,19 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams* wf_in, co
             }
             for (int b = 0; b < max_bounces && e == hipSuccess; b++) {
                 wf.bounce = b;
-                if (packet && b == 0)
-                    e = launch_extend_primary<4, kLdsBlock>(kb, wf, (int)nseg, lds_bytes_in_lds(img, 4) + 32, bs);
-                else if (in_lds)
-                    e = launch_extend<true, 4, kLdsBlock>(kb, wf, (int)nseg, lds_bytes_in_lds(img, 4) + 32, bs);
-                else
-                    e = launch_extend<false, MCPT_WF_GLOBAL_S, kGlobalBlock>(kb, wf, (int)nseg,
+                const size_t llds = in_lds ? wf_lds_extend_bytes(kb.scene) : 0;
+                if (packet && b == 0) {
+                    if constexpr (MCPT_WF_HYBRID)
+                        e = launch_extend_primary<kLayHybrid, kHybridS, kHybridBlock>(kb, wf, (int)nseg, llds, bs);
+                    else
+                        e = launch_extend_primary<kLayLds, 4, kLdsBlock>(kb, wf, (int)nseg, llds, bs);
+                } else if (in_lds) {
+                    if constexpr (MCPT_WF_HYBRID)
+                        e = launch_extend<kLayHybrid, kHybridS, kHybridBlock>(kb, wf, (int)nseg, llds, bs);
+                    else
+                        e = launch_extend<kLayLds, 4, kLdsBlock>(kb, wf, (int)nseg, llds, bs);
+                } else
+                    e = launch_extend<kLayGlobal, MCPT_WF_GLOBAL_S, kGlobalBlock>(kb, wf, (int)nseg,
                                                                             (size_t)MCPT_WF_GLOBAL_S * kGlobalBlock * 16 + 32,
                                                               bs);
                 if (e != hipSuccess) break;
