@@ -321,6 +321,18 @@ constexpr int kWfLdsCap = MCPT_KD_GROUPS ? MCPT_WF_GROUP_CAP : MCPT_WF_DESCENT_C
 #ifndef MCPT_WF_GLOBAL_MINWG
 #define MCPT_WF_GLOBAL_MINWG 6
 #endif
+// register budgets (waves per SIMD the compiler plans for; 0 = none) of the
+// LDS scenes' lean extend and of the queue-order shade, and the shade's
+// workgroup beside an LDS extend workgroup (512: two waves per SIMD)
+#ifndef MCPT_WF_LDS_WPE
+#define MCPT_WF_LDS_WPE 0
+#endif
+#ifndef MCPT_WF_SHADE_WPE
+#define MCPT_WF_SHADE_WPE 0
+#endif
+#ifndef MCPT_WF_SHADE_LDS_BLOCK
+#define MCPT_WF_SHADE_LDS_BLOCK 512
+#endif
 #ifndef MCPT_WF_GEO_LDS
 #define MCPT_WF_GEO_LDS 1
 #endif
@@ -340,7 +352,9 @@ constexpr int kLayGlobal = 0, kLayLds = 1, kLayHybrid = 2;
 template <int LAY, int S, int BLOCK, bool COUNT, bool SORT>
 __global__ void __launch_bounds__(BLOCK, (LAY == kLayGlobal && !COUNT && !SORT && MCPT_WF_GLOBAL_MINWG)
                                              ? MCPT_WF_GLOBAL_MINWG
-                                             : (LAY == kLayHybrid ? 6 : 1))   // (waves per SIMD)
+                                             : (LAY == kLayHybrid ? 6
+                                                : (LAY == kLayLds && !COUNT && !SORT && MCPT_WF_LDS_WPE
+                                                       ? MCPT_WF_LDS_WPE : 1)))   // (waves per SIMD)
 wf_extend(const KernelParams kp, const WfParams wf) {
     constexpr bool IN_LDS = LAY != kLayGlobal;            // node words in LDS
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -872,7 +886,8 @@ __global__ void __launch_bounds__(kShadeBlock) wf_shade(const KernelParams kp, c
 // LDS atomic per wave, 64 consecutive slots), so queue b+1 is dense.  Queue
 // order is scheduling-dependent, but nothing reads it (state keyed by pid).
 template <int BLOCK, bool GEO_LDS>
-__global__ void __launch_bounds__(BLOCK) wf_shade_slots(const KernelParams kp, const WfParams wf) {
+__global__ void __launch_bounds__(BLOCK, MCPT_WF_SHADE_WPE ? MCPT_WF_SHADE_WPE : 1)
+wf_shade_slots(const KernelParams kp, const WfParams wf) {
     const uint32_t g = blockIdx.x;
     if (g >= wf.nseg) return;
     __shared__ uint32_t lnext;
@@ -1162,8 +1177,9 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams* wf_in, co
                     hipLaunchKernelGGL(wf_shade, dim3(nseg * per), dim3(kShadeBlock), 0, bs, kb, wf, per);
                 else if (in_lds && ns == 1)   // alone on the GPU: 16 waves per segment keep HBM busy
                     hipLaunchKernelGGL(shade_kernel<1024>(geo_bytes != 0), dim3(nseg), dim3(1024), geo_bytes, bs, kb, wf);
-                else if (in_lds)              // beside an extend workgroup: 8 waves (2 x 64 VGPRs per SIMD)
-                    hipLaunchKernelGGL(shade_kernel<512>(geo_bytes != 0), dim3(nseg), dim3(512), geo_bytes, bs, kb, wf);
+                else if (in_lds)              // beside an extend workgroup: 8 waves (2 x 80 VGPRs per SIMD)
+                    hipLaunchKernelGGL(shade_kernel<MCPT_WF_SHADE_LDS_BLOCK>(geo_bytes != 0), dim3(nseg),
+                                       dim3(MCPT_WF_SHADE_LDS_BLOCK), geo_bytes, bs, kb, wf);
                 else
                     hipLaunchKernelGGL(shade_kernel<256>(geo_bytes != 0), dim3(nseg), dim3(256), geo_bytes, bs, kb, wf);
                 e = hipGetLastError();
