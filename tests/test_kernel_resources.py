@@ -78,6 +78,16 @@ def test_shipped_kernels_fit_16_waves_per_cu(tmp_path):
         # product variants: the DBG unit-counter megakernels (template arg 4 true) may spill
         if "wf_extend" in name or re.search(r"path_kernelILb[01]ELi\d+ELi\d+ELb0E", name):
             assert r["scratch"] == 0, (name, r)
+    # the residency the wavefront's schedule is built on: the
+    # lean queue-order extend of global-memory scenes (template <LAY 0, S, 256,
+    # lean, queue order>) at <= 80 VGPRs -- six workgroups per CU -- and the LDS
+    # scenes' (LAY 1) at <= 88 beside two <= 80-VGPR shade waves per SIMD
+    g_lean = [r for k, r in extend.items() if re.search(r"wf_extendILi0ELi\d+ELi256ELb0ELb0E", k)]
+    l_lean = [r for k, r in extend.items() if re.search(r"wf_extendILi1ELi4ELi1024ELb0ELb0E", k)]
+    assert len(g_lean) == 1 and len(l_lean) == 1, sorted(extend)
+    assert g_lean[0]["vgpr"] <= 80 and l_lean[0]["vgpr"] <= 88, (g_lean, l_lean)
+    shade = [r for k, r in kernels.items() if re.search(r"wf_shade_slotsILi512E", k)]
+    assert shade and all(r["vgpr"] <= 80 for r in shade), shade
     # the other wavefront kernels run at most 512 VGPRs' worth of waves; keep them spill-free
     for name, r in kernels.items():
         if "wf_" in name:
