@@ -45,6 +45,11 @@ constexpr int kHybridBlock = 768, kHybridS = 2, kHybridPerCu = 2;
 constexpr int kLdsBlock = 1024;          // in-LDS variant: one 16-wave workgroup per CU
 constexpr int kGlobalBlock = 256;        // global variant
 constexpr int kGlobalBlocksPerCu = 4;
+// the wavefront extend's segments (workgroups) per CU for global-memory scenes
+#ifndef MCPT_WF_GLOBAL_SEGS
+#define MCPT_WF_GLOBAL_SEGS 4
+#endif
+constexpr int kWfGlobalSegsPerCu = MCPT_WF_GLOBAL_SEGS;
 constexpr size_t kMaxLds = 160 * 1024;   // gfx950 LDS per CU
 
 struct GpuGeom {

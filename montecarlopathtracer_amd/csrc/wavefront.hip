@@ -1063,7 +1063,7 @@ void read_lane_use_wf(unsigned long long out[6]) {   // wavefront extend lane-us
 #endif
 
 int wavefront_segments(const GpuScene& sc, int cus) {
-    return wf_in_lds(sc) ? (MCPT_WF_HYBRID ? kHybridPerCu * cus : cus) : cus * kGlobalBlocksPerCu;
+    return wf_in_lds(sc) ? (MCPT_WF_HYBRID ? kHybridPerCu * cus : cus) : cus * kWfGlobalSegsPerCu;
 }
 // LDS bytes of an LDS-scene extend workgroup: stack + image (or its part from the nodes on) + counters
 size_t wf_lds_extend_bytes(const GpuScene& sc) {
@@ -1132,7 +1132,7 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams* wf_in, co
             // the shade's material table in LDS if it fits beside the extend's
             // workgroups on a CU (MCPT_WF_GEO_LDS)
             const size_t ext_lds = in_lds ? (MCPT_WF_HYBRID ? kHybridPerCu : 1) * wf_lds_extend_bytes(kp.scene)
-                                          : (size_t)kGlobalBlocksPerCu * (MCPT_WF_GLOBAL_S * kGlobalBlock * 16 + 32);
+                                          : (size_t)kWfGlobalSegsPerCu * (MCPT_WF_GLOBAL_S * kGlobalBlock * 16 + 32);
             const size_t geo_bytes = (MCPT_WF_GEO_LDS && ext_lds + 64 * (size_t)kp.scene.n_geoms + 64 <= kLdsPerCu)
                                          ? 64 * (size_t)kp.scene.n_geoms : 0;
             // LDS scenes: one 8x8 tile of one sample per group; global-memory
