@@ -321,6 +321,9 @@ constexpr int kWfLdsCap = MCPT_KD_GROUPS ? MCPT_WF_GROUP_CAP : MCPT_WF_DESCENT_C
 #ifndef MCPT_WF_GLOBAL_MINWG
 #define MCPT_WF_GLOBAL_MINWG 6
 #endif
+#ifndef MCPT_WF_GLOBAL_PREFETCH
+#define MCPT_WF_GLOBAL_PREFETCH 1
+#endif
 // register budgets (waves per SIMD the compiler plans for; 0 = none) of the
 // LDS scenes' lean extend and of the queue-order shade, and the shade's
 // workgroup beside an LDS extend workgroup (512: two waves per SIMD)
@@ -411,8 +414,12 @@ wf_extend(const KernelParams kp, const WfParams wf) {
     RayState r;
     r.htri = -1;
     int mode = kDead;
+    // PF: the next ray of every lane is loaded a whole burst ahead (no4/nd4);
+    // without it (MCPT_WF_GLOBAL_PREFETCH = 0, global-memory scenes only) a
+    // finished lane loads its next ray in the hand-off, 8 VGPRs fewer
+    constexpr bool PF = LAY != kLayGlobal || MCPT_WF_GLOBAL_PREFETCH;
     uint32_t slot = cur_chunk.take(true, lcnt + 4), depth = 0;
-    uint32_t nslot = cur_chunk.take(true, lcnt + 4);
+    uint32_t nslot = PF ? cur_chunk.take(true, lcnt + 4) : 0u;
     float4 no4 = make_float4(0, 0, 0, 0), nd4 = make_float4(0, 0, 0, 0);
     auto start = [&](float4 o4, float4 d4) {
         // opaque copies: the loop below must not see its ray registers as
@@ -443,7 +450,7 @@ wf_extend(const KernelParams kp, const WfParams wf) {
     const float4 eye4 = make_float4(kp.eye[0], kp.eye[1], kp.eye[2], 0.0f);
     auto ld_o = [&](uint32_t sl) { return eye0 ? eye4 : ldq(&qb[qf(seg0 + sl, kQO, qs)]); };
     if (slot < count) start(ld_o(slot), ldq(&qb[qf(seg0 + slot, kQD, qs)]));
-    if (nslot < count) { no4 = ld_o(nslot); nd4 = ldq(&qb[qf(seg0 + nslot, kQD, qs)]); }
+    if (PF && nslot < count) { no4 = ld_o(nslot); nd4 = ldq(&qb[qf(seg0 + nslot, kQD, qs)]); }
     WF_STAMP(tm_setup);
     for (;;) {
         // ---- traversal burst until enough lanes are done ---------------------
@@ -475,9 +482,12 @@ wf_extend(const KernelParams kp, const WfParams wf) {
         // live across the burst -- a dead load destination is reused by the
         // loop, which must then wait for the load first (a vmcnt wait in every
         // burst's first iteration: C2 +0.9%, C4 +2.8% without it).
-        no4 = make_float4(opaque(no4.x), opaque(no4.y), opaque(no4.z), opaque(no4.w));
-        nd4 = make_float4(opaque(nd4.x), opaque(nd4.y), opaque(nd4.z), opaque(nd4.w));
+        if constexpr (PF) {
+            no4 = make_float4(opaque(no4.x), opaque(no4.y), opaque(no4.z), opaque(no4.w));
+            nd4 = make_float4(opaque(nd4.x), opaque(nd4.y), opaque(nd4.z), opaque(nd4.w));
+        }
         const bool fin = mode == kReady;
+        const uint32_t ns0 = PF ? 0u : cur_chunk.take(fin, lcnt + 4);   // (collective: every lane)
         uint32_t cls = 4u;
         const uint32_t fslot = slot;
         float4 hrec = make_float4(0, 0, 0, 0);
@@ -493,9 +503,16 @@ wf_extend(const KernelParams kp, const WfParams wf) {
             }
             // (the next ray set up unconditionally: no branch in the hand-off; a
             // lane past the segment's end runs on its stale prefetch, then dies)
-            slot = nslot;
-            start(no4, nd4);
-            if (nslot >= count) mode = kDead;
+            if constexpr (PF) {
+                slot = nslot;
+                start(no4, nd4);
+            } else {
+                slot = ns0;
+                float4 o4 = make_float4(0, 0, 0, 0), d4 = make_float4(0, 0, 0, __uint_as_float(kNoRay));
+                if (slot < count) { o4 = ld_o(slot); d4 = ldq(&qb[qf(seg0 + slot, kQD, qs)]); }
+                start(o4, d4);
+            }
+            if (slot >= count) mode = kDead;
             if constexpr (MCPT_WF_HIT_ID && !SORT)   // (r holds the next ray by now: the id from hrec)
                 reinterpret_cast<int32_t*>(qb + qf(0, kQHIT, qs))[seg0 + fslot] = __float_as_int(hrec.w);
             else if constexpr ((MCPT_WF_NT & 4) != 0 || (!IN_LDS && MCPT_WF_NT_HIT_GLOBAL))
@@ -509,11 +526,13 @@ wf_extend(const KernelParams kp, const WfParams wf) {
                 out[k].append(cls == k, fslot, lcnt + k, wf.cls_list + (size_t)k * wf.slot_stride + seg0);
         }
         // ---- prefetch the next ray of every lane that just started one -------
-        const bool want = fin && mode != kDead;
-        const uint32_t ns = cur_chunk.take(want, lcnt + 4);
-        if (want) {
-            nslot = ns;
-            if (nslot < count) { no4 = ld_o(nslot); nd4 = ldq(&qb[qf(seg0 + nslot, kQD, qs)]); }
+        if constexpr (PF) {
+            const bool want = fin && mode != kDead;
+            const uint32_t ns = cur_chunk.take(want, lcnt + 4);
+            if (want) {
+                nslot = ns;
+                if (nslot < count) { no4 = ld_o(nslot); nd4 = ldq(&qb[qf(seg0 + nslot, kQD, qs)]); }
+            }
         }
         WF_STAMP(tm_hand);
         if (!__ballot(mode != kDead)) break;
