@@ -707,31 +707,47 @@ __global__ void __launch_bounds__(BLOCK, LAY == kLayHybrid ? 6 : 1) wf_extend_pr
                     const uint4 pr = *reinterpret_cast<const uint4*>(nodes + left);   // first pair)
                     const int a = (int)(w0 >> 30);
                     const float sv = __uint_as_float(w1);
-                    const float oa = sel3(a, eye.x, eye.y, eye.z);
+                    const float oa = sel3(a, eye.x, eye.y, eye.z);   // wave-uniform (common origin)
                     const float ia = sel3(a, r.ix, r.iy, r.iz);
                     const float t = (sv - oa) * ia;
-                    const bool on_plane = oa == sv;            // wave-uniform (common origin)
-                    bool below = oa < sv, pp = false;
-                    if (on_plane) {
-                        const float da = sel3(a, r.d.x, r.d.y, r.d.z);
-                        below = da <= 0.0f;
-                        pp = da == 0.0f;
-                    }
                     const float te = t * kEpsHi;
                     const bool no = !(t > 0.0f) | (t > r.tmax);
                     const bool fo = te < r.tmin;
-                    const bool go_far = !pp & !no & fo;
-                    const bool push_it = pp | (!pp & !no & !fo);
-                    const bool need_near = active & !go_far, need_far = active & (go_far | push_it);
-                    const float near_max = push_it ? min_qnan(te, r.tmax) : r.tmax;   // near: [tmin, near_max]
-                    const float far_min = go_far ? r.tmin : max_qnan(t, r.tmin);      // far: [far_min, tmax]
-                    // the wave's order: left first iff the (common) near side is the left
-                    const bool first_left = on_plane | (oa < sv);
-                    const bool near_first = below == first_left;
-                    const bool need1 = near_first ? need_near : need_far;
-                    const bool need2 = near_first ? need_far : need_near;
-                    const float lo1 = near_first ? r.tmin : far_min, hi1 = near_first ? near_max : r.tmax;
-                    const float lo2 = near_first ? far_min : r.tmin, hi2 = near_first ? r.tmax : near_max;
+                    bool first_left, need1, need2;
+                    float lo1, hi1, lo2, hi2;
+                    if (__builtin_expect(oa != sv, 1)) {
+                        // (a uniform branch) the origin is off the plane: every lane's
+                        // near side is the wave's first child, below == first_left,
+                        // and no lane lies in the plane (pp false)
+                        first_left = oa < sv;
+                        const bool go_far = !no & fo, both = !no & !fo;
+                        need1 = active & !go_far;
+                        need2 = active & (go_far | both);
+                        // (both interval ends computed unconditionally: a select of the
+                        // asm min/max, not a branch around it)
+                        const float mn = min_qnan(te, r.tmax), mx = max_qnan(t, r.tmin);
+                        lo1 = r.tmin;
+                        hi1 = both ? mn : r.tmax;
+                        lo2 = go_far ? r.tmin : mx;
+                        hi2 = r.tmax;
+                    } else {
+                        // the origin on the plane: the near side by each lane's direction
+                        const float da = sel3(a, r.d.x, r.d.y, r.d.z);
+                        const bool below = da <= 0.0f, pp = da == 0.0f;
+                        const bool go_far = !pp & !no & fo;
+                        const bool push_it = pp | (!pp & !no & !fo);
+                        const bool need_near = active & !go_far, need_far = active & (go_far | push_it);
+                        const float near_max = push_it ? min_qnan(te, r.tmax) : r.tmax;   // near: [tmin, near_max]
+                        const float far_min = go_far ? r.tmin : max_qnan(t, r.tmin);      // far: [far_min, tmax]
+                        // the wave's order: left first (the near side of every lane not in the plane)
+                        first_left = true;
+                        need1 = below ? need_near : need_far;
+                        need2 = below ? need_far : need_near;
+                        lo1 = below ? r.tmin : far_min;
+                        hi1 = below ? near_max : r.tmax;
+                        lo2 = below ? far_min : r.tmin;
+                        hi2 = below ? r.tmax : near_max;
+                    }
                     const uint32_t f0 = first_left ? pr.x : pr.z, f1 = first_left ? pr.y : pr.w;
                     const uint32_t s0 = first_left ? pr.z : pr.x, s1 = first_left ? pr.w : pr.y;
                     if (__ballot(need1)) {
