@@ -152,3 +152,23 @@ def test_edge_scene_matches_oracle(mcpt, oracle_mod, edge_scene, layout):
             assert st[k] == rc[k], (kind, layout, pipe, k, st[k], rc[k])
         for k in ("rays", "paths", "shades"):
             assert st[k] == bc[k], (kind, layout, pipe, k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pipeline", ["megakernel", "wavefront", "wavefront-sorted"])
+def test_edge_scene_quinengine_mode_matches_oracle(mcpt, oracle_mod, edge_scene, pipeline):
+    """The same scenes under rtx.hlsl semantics (roulette, 3x depth cap, QE
+    camera and accumulation), LDS layout."""
+    kind, path = edge_scene
+    depth, seed = 5, 0x5EED
+    ref, rc = oracle_mod.Scene(path).render(oracle_mod.RenderParams(
+        width=W, height=H, spp=SPP, spp_chunk=CHUNK, max_depth=depth, seed=seed, illum=1.0, fov=45.0,
+        fresnel_kd=0, threads=min(os.cpu_count() or 8, 16), mode=oracle_mod.MODE_QE))
+    scene = mcpt.Scene(mcpt.ObjModel(path))
+    img, st = scene.render(mcpt.RenderParams.for_quinengine(
+        width=W, height=H, spp=SPP, spp_chunk=CHUNK, max_depth=depth, seed=seed,
+        pipeline="wavefront" if pipeline.startswith("wavefront") else pipeline, wf_sort=pipeline == "wavefront-sorted"))
+    assert float(ref.max()) > 0.0, kind
+    assert np.array_equal(img.view(np.uint32), ref.view(np.uint32)), (kind, pipeline)
+    for k in COUNTS:
+        assert st[k] == rc[k], (kind, pipeline, k, st[k], rc[k])
