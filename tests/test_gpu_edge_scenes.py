@@ -172,3 +172,39 @@ def test_edge_scene_quinengine_mode_matches_oracle(mcpt, oracle_mod, edge_scene,
     assert np.array_equal(img.view(np.uint32), ref.view(np.uint32)), (kind, pipeline)
     for k in COUNTS:
         assert st[k] == rc[k], (kind, pipeline, k, st[k], rc[k])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", ["auto", "global"])
+def test_edge_scene_device_hits(mcpt, oracle_mod, edge_scene, layout):
+    """mcpt_intersect on tests/_raysets.py's adversarial families over these
+    scenes: the oracle walk's hits and counters bit for bit, and the brute
+    force's off the triangle-edge origins (family 5)."""
+    import warnings
+    from _raysets import ray_sets
+    kind, path = edge_scene
+    if kind == "tiny":
+        pytest.skip("one leaf, no split planes for family 4")
+    scene = mcpt.Scene(mcpt.ObjModel(path), layout=layout)
+    boxes = int(scene.info()["node_boxes"])
+    o_s = oracle_mod.Scene(path)
+    n = 40_000
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", RuntimeWarning)     # point triangles: zero directions, dropped
+        o, d = ray_sets(o_s, n, seed=29)
+    tri, hit, st = scene.intersect(o, d)
+    tk, _, hk, ck = o_s.intersect(o, d, oracle_mod.KD_ORDERED, node_boxes=boxes, threads=8)
+    assert np.array_equal(tri, tk)
+    hit_k = np.where(tk[:, None] >= 0, hk[:, :3], 0.0).astype(np.float32)
+    hit_g = np.where(tri[:, None] >= 0, hit, 0.0).astype(np.float32)
+    assert np.array_equal(hit_g.view(np.uint32), hit_k.view(np.uint32))
+    for k in ("inner_visits", "leaf_visits", "leaf_refs", "tri_tests"):
+        assert st[k] == ck[k], (k, st[k], ck[k])
+    tb, _, hb, _ = o_s.intersect(o, d, oracle_mod.BRUTE, threads=8)
+    k5 = n // 8
+    fam5 = np.zeros(o.shape[0], bool)
+    fam5[6 * k5:7 * k5] = True
+    bad = np.nonzero((tb != tri) | (np.where(tb[:, None] >= 0, hb[:, :3], 0.0).astype(np.float32).view(np.uint32)
+                                    != hit_g.view(np.uint32)).any(axis=1))[0]
+    assert not (~fam5[bad]).any(), bad[~fam5[bad]][:10]
+    assert (tri >= 0).mean() > 0.3
