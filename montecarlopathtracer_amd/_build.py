@@ -16,7 +16,10 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIBDIR, os.environ.get("MCPT_LIB_NAME", "libmcpt.so"))
-SOURCES = ["host_model.cpp", "kd_cache.cpp", "capi.cpp", "render.hip", "wavefront.hip"]
+SOURCES = ["host_model.cpp", "kd_cache.cpp", "capi.cpp", "render.hip", "wavefront.hip", "wavefront_primary.hip"]
+# per-source code generation (wavefront_primary.hip: the bounce-0 packet extend's
+# wave-uniform control flow as scalar branches)
+SOURCE_FLAGS = {"wavefront_primary.hip": ["-mllvm", "-structurizecfg-skip-uniform-regions=1"]}
 HEADERS = ["host_model.hpp", "mcpt_device.hpp", "render_launch.hpp", "trace_device.hpp", "half_box.hpp"]
 ARCH = os.environ.get("MCPT_OFFLOAD_ARCH", "gfx950")
 
@@ -53,7 +56,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         lang = (["-x", "hip", f"--offload-arch={ARCH}", "-mllvm", f"-amdgpu-sched-strategy={sched}"]
                 if src.endswith(".hip")
                 else ["-x", "c++", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include"])
-        cmd = [hipcc] + lang + COMMON + ["-c", os.path.join(CSRC, src), "-o", obj]
+        cmd = [hipcc] + lang + COMMON + SOURCE_FLAGS.get(src, []) + ["-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         r = subprocess.run(cmd, capture_output=True, text=True)

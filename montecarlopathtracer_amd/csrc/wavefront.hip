@@ -41,6 +41,15 @@
 #include "trace_device.hpp"
 
 
+// MCPT_WF_PRIMARY_TU = 1 (wavefront_primary.hip): this file compiled for the
+// bounce-0 packet extend alone, in a translation unit of its own so that it
+// can take its own code-generation flags (_build.py: its wave-uniform control
+// flow left unstructurized); every other kernel and the host launch code are
+// compiled here with MCPT_WF_PRIMARY_TU = 0.
+#ifndef MCPT_WF_PRIMARY_TU
+#define MCPT_WF_PRIMARY_TU 0
+#endif
+
 namespace mcpt {
 
 using namespace dev;
@@ -200,6 +209,7 @@ __host__ __device__ __forceinline__ bool implicit0(const KernelParams& kp, const
 static_assert(MCPT_WF_SOA || !MCPT_WF_HIT_ID, "hit ids use the SoA hit stream");
 static_assert(MCPT_WF_HIT_ID && MCPT_WF_SOA, "capi.cpp wf_layout: queue-order queues hold 4-B hit ids, SoA");
 
+#if !MCPT_WF_PRIMARY_TU
 // ---- generate: primary rays of the batch (CUTracer.cu:186-211) -------------
 // Paths go to segments in groups of 2^group_shift (64 = one 8x8 tile of one
 // sample: a coherent wave of primary rays), group j -> segment j % nseg, so
@@ -283,6 +293,8 @@ struct ClassBuf {
     }
 };
 
+#endif  // !MCPT_WF_PRIMARY_TU
+
 // Issue priority of the extend's traversal bursts (its hand-off runs one
 // higher); the co-resident shade runs at 0.
 #ifndef MCPT_WF_EXT_PRIO
@@ -343,6 +355,7 @@ constexpr size_t kLdsPerCu = 160 * 1024;
 constexpr int kLayGlobal = 0, kLayLds = 1, kLayHybrid = 2;
 
 
+#if !MCPT_WF_PRIMARY_TU
 // ---- extend: closest hit of every ray of this workgroup's segment -----------
 // COUNT = false (lean renders): the traversal counters are compiled out.
 // SORT = WfParams::sort, a template argument so that the queue-order variant
@@ -562,6 +575,8 @@ wf_extend(const KernelParams kp, const WfParams wf) {
     __syncthreads();
     if (tid < 4) cn->cls[tid] = lcnt[tid];
 }
+
+#endif  // !MCPT_WF_PRIMARY_TU
 
 // ---- extend of bounce 0, wave-coherent (CV mode, queue-order shade) ---------
 // Primary rays share the eye as their origin, and generate deals them in
@@ -839,6 +854,7 @@ __global__ void __launch_bounds__(BLOCK, LAY == kLayHybrid ? 6 : 1) wf_extend_pr
     if (tid < 4) cn->cls[tid] = 0;
 }
 
+#if !MCPT_WF_PRIMARY_TU
 // ---- shade: each segment's class lists back to back (CUTracer.cu:105-175) ---
 // Items of segment g are taken in the order [diffuse, phong, fresnel,
 // terminate]; the i-th continuing item writes its next ray to slot i of the
@@ -1057,6 +1073,7 @@ __global__ void __launch_bounds__(256) wf_accumulate(const KernelParams kp, cons
     kp.partial[(size_t)(wf.chunk_index + j) * kp.npix_local + wf.v0 + u] = make_float4(part.x, part.y, part.z, 0.0f);
 }
 
+#endif  // !MCPT_WF_PRIMARY_TU
 
 template <int LAY, int S, int BLOCK>
 hipError_t launch_extend_primary(const KernelParams& kp, const WfParams& wf, int grid, size_t lds, hipStream_t st) {
@@ -1068,6 +1085,7 @@ hipError_t launch_extend_primary(const KernelParams& kp, const WfParams& wf, int
     return hipGetLastError();
 }
 
+#if !MCPT_WF_PRIMARY_TU
 template <int BLOCK>
 auto shade_kernel(bool geo_lds) { return geo_lds ? wf_shade_slots<BLOCK, true> : wf_shade_slots<BLOCK, false>; }
 
@@ -1087,7 +1105,22 @@ hipError_t launch_extend(const KernelParams& kp, const WfParams& wf, int grid, s
 // child-box pair records (node_boxes) is always read from global memory
 bool wf_in_lds(const GpuScene& sc) { return !sc.node_boxes && lds_bytes_in_lds(sc.image_bytes, 4) + 32 <= kMaxLds; }
 
+#endif  // !MCPT_WF_PRIMARY_TU
 }  // namespace
+
+#if MCPT_WF_PRIMARY_TU
+// the bounce-0 packet extend's launch, called by launch_wavefront (the other
+// translation unit)
+hipError_t launch_wavefront_primary(const KernelParams& kp, const WfParams& wf, int grid, size_t lds,
+                                    hipStream_t st) {
+    if constexpr (MCPT_WF_HYBRID)
+        return launch_extend_primary<kLayHybrid, kHybridS, kHybridBlock>(kp, wf, grid, lds, st);
+    else
+        return launch_extend_primary<kLayLds, 4, kLdsBlock>(kp, wf, grid, lds, st);
+}
+#else
+hipError_t launch_wavefront_primary(const KernelParams& kp, const WfParams& wf, int grid, size_t lds,
+                                    hipStream_t st);   // wavefront_primary.hip
 
 #ifdef MCPT_PHASE_TIMING
 void read_lane_use_wf(unsigned long long out[6]) {   // wavefront extend lane-use counters, then reset
@@ -1194,10 +1227,7 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams* wf_in, co
                 wf.bounce = b;
                 const size_t llds = in_lds ? wf_lds_extend_bytes(kb.scene) : 0;
                 if (packet && b == 0) {
-                    if constexpr (MCPT_WF_HYBRID)
-                        e = launch_extend_primary<kLayHybrid, kHybridS, kHybridBlock>(kb, wf, (int)nseg, llds, bs);
-                    else
-                        e = launch_extend_primary<kLayLds, 4, kLdsBlock>(kb, wf, (int)nseg, llds, bs);
+                    e = launch_wavefront_primary(kb, wf, (int)nseg, llds, bs);
                 } else if (in_lds) {
                     if constexpr (MCPT_WF_HYBRID)
                         e = launch_extend<kLayHybrid, kHybridS, kHybridBlock>(kb, wf, (int)nseg, llds, bs);
@@ -1236,5 +1266,6 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams* wf_in, co
     if (variant_out) *variant_out = in_lds ? 4 : 5;
     return e;
 }
+#endif  // MCPT_WF_PRIMARY_TU
 
 }  // namespace mcpt

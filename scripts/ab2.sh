@@ -17,7 +17,9 @@ for lib in $LIBS; do
 import json, sys
 ln = [json.loads(x) for x in open(sys.argv[1]) if x.startswith("{")][-1]
 alt = ln.get("other_pipeline") or {}
-print(f"{sys.argv[2]}: wf {ln['value']/1e3:.3f} G rays/s ({ln['kernel_ms_avg']} ms)  mk {alt.get('value', 0)/1e3:.3f} ({alt.get('kernel_ms_avg')})")
+c4 = (ln.get("extra_lines") or {}).get("c4") or {}
+print(f"{sys.argv[2]}: wf {ln['value']/1e3:.3f} G rays/s ({ln['kernel_ms_avg']} ms)  mk {alt.get('value', 0)/1e3:.3f} ({alt.get('kernel_ms_avg')})"
+      + (f"  c4 {c4['value']/1e3:.3f}" if "value" in c4 else ""))
 PY
 done
 done
