@@ -340,28 +340,46 @@ def host_cores() -> int:
     return max(1, min(n, int(os.environ.get("OMP_NUM_THREADS", "16"))))
 
 
-def c4_line(args) -> dict:
-    """BASELINE configs[3] (C4: the seeded 70k-triangle mesh in scene01's box,
-    1024x1024 @ 1024 spp, scene image in global memory with the child-box
-    cull) timed the same way, in a child process of this bench (its own GPU
-    context; this process's workspace stays allocated beside it)."""
+def child_line(args, scene: str, spp: int, steps: int, warmup: int, tag: str) -> dict:
+    """Another BASELINE configuration timed the same way (same pipeline, PMC
+    roofline passes) in a child process of this bench (its own GPU context;
+    this process's workspace stays allocated beside it)."""
     import subprocess
-    cmd = [sys.executable, os.path.abspath(__file__), "--scene", "cornell_bunny70k", "--no-c4", "--no-alt",
-           "--no-cpu-baseline", "--steps", str(args.steps), "--warmup", str(args.warmup),
-           "--width", str(args.width), "--height", str(args.height), "--spp", str(args.spp),
+    cmd = [sys.executable, os.path.abspath(__file__), "--scene", scene, "--no-extra", "--no-alt",
+           "--no-cpu-baseline", "--steps", str(steps), "--warmup", str(warmup),
+           "--width", str(args.width), "--height", str(args.height), "--spp", str(spp),
            "--spp-chunk", str(args.spp_chunk), "--pipeline", args.pipeline] + (["--no-pmc"] if args.no_pmc else []) + \
-        (["--keep-pmc", os.path.join(args.keep_pmc, "c4")] if args.keep_pmc else [])
+        (["--keep-pmc", os.path.join(args.keep_pmc, tag)] if args.keep_pmc else [])
     env = dict(os.environ)
     for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
     try:
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
     except subprocess.TimeoutExpired:
-        return {"error": "C4 child timed out"}
+        return {"error": f"{tag} child timed out"}
     lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
     if r.returncode != 0 or not lines:
-        return {"error": f"C4 child rc {r.returncode}: {r.stderr[-400:]}"}
+        return {"error": f"{tag} child rc {r.returncode}: {r.stderr[-400:]}"}
     return json.loads(lines[-1])
+
+
+def c4_line(args) -> dict:
+    """BASELINE configs[3] (C4: the seeded 70k-triangle mesh in scene01's box,
+    1024x1024 @ 1024 spp, scene image in global memory with the child-box
+    cull), the same steps and warmup as the line."""
+    return child_line(args, "cornell_bunny70k", args.spp, args.steps, args.warmup, "c4")
+
+
+def c5_line(args) -> dict:
+    """BASELINE configs[4] (C5: the wavefront pipeline at 4096 spp -- per-bounce
+    compaction of live rays into the next queue; the shade runs in queue order,
+    the material-sorted shade (wf_sort = 1) renders the same image slower,
+    DESIGN.md 5b) on ONE GPU: configs[4] names 8 GPUs, which the driver's
+    node runs as the main line's N = 8 shares; 3-5 steps (a step is ~1 s)."""
+    line = child_line(args, "scene01", 4 * args.spp, max(3, min(args.steps, 5)), 1, "c5")
+    if "config" in line:
+        line["config"]["shade"] = "queue order (per-bounce compaction by LDS-atomic append); wf_sort=1: same image"
+    return line
 
 
 def main():
@@ -404,10 +422,16 @@ def main():
     ap.add_argument("--no-c4", action="store_true",
                     help="N = 1: skip the C4 line (BASELINE configs[3], the 70k-triangle mesh in the Cornell box, "
                          "same pipeline, steps and PMC roofline) reported under extra_lines.c4")
+    ap.add_argument("--no-c5", action="store_true",
+                    help="N = 1: skip the C5 line (BASELINE configs[4], the wavefront at 4096 spp on one GPU, "
+                         "3-5 steps, PMC roofline) reported under extra_lines.c5")
+    ap.add_argument("--no-extra", action="store_true", help="skip both extra lines (--no-c4 --no-c5)")
     ap.add_argument("--counting", action="store_true", help="time the counting megakernel instead of the lean one")
     ap.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 PMC passes (HBM bytes, VALU issue)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)   # one render under rocprofv3
     args = ap.parse_args()
+    if args.no_extra:
+        args.no_c4 = args.no_c5 = True
 
     import torch
     import torch.distributed as dist
@@ -676,8 +700,14 @@ def main():
             "cpu_baseline": None,
             "other_pipeline": alt,
         }
-        if n_gpus == 1 and not args.no_c4 and args.scene == "scene01":
-            line["extra_lines"] = {"c4": c4_line(args)}
+        if n_gpus == 1 and args.scene == "scene01":
+            extra = {}
+            if not args.no_c4:
+                extra["c4"] = c4_line(args)
+            if not args.no_c5 and args.spp == 1024 and args.pipeline == "wavefront":
+                extra["c5"] = c5_line(args)
+            if extra:
+                line["extra_lines"] = extra
         if n_gpus == 1 and not args.no_cpu_baseline:
             # the GPU's own C1 frame, for the ray-count check of the CPU run
             s1 = scene if args.scene == "scene01" else M.Scene(M.ObjModel(M.scene_path("scene01")))

@@ -241,10 +241,9 @@ struct DeviceOrder {
     std::vector<uint32_t> leaf_order;   // host leaf nodes in device order
     std::vector<uint32_t> tri_order;    // device triangle slot -> kd id
     std::vector<uint32_t> tri_new;      // kd id -> device triangle slot
-    std::vector<uint8_t> group_root;    // device_order_groups: node is a group root (empty: no groups)
 };
 
-// leaves in device node order, triangles by first appearance (both layouts)
+// leaves in device node order, triangles by first appearance
 void order_leaves(const mcpt::HostScene& hs, DeviceOrder& d) {
     const uint32_t nn = static_cast<uint32_t>(hs.nodes.size());
     std::vector<uint32_t> by_dev(d.n_slots, 0xFFFFFFFFu);
@@ -303,54 +302,6 @@ DeviceOrder device_order(const mcpt::HostScene& hs) {
     return d;
 }
 
-// Two-level node groups (8-B node images, MCPT_KD_GROUPS; trace_device.hpp
-// descend_steps): every inner node at even depth is a group root; its group
-// is its sibling pair followed by the pairs of its inner children (left
-// child's first), so the walk reads both levels below a root with one 48-B
-// read.  Groups are emitted breadth-first (the top of the tree first).  The
-// pair count -- hence the image size -- is the cluster order's.
-DeviceOrder device_order_groups(const mcpt::HostScene& hs) {
-    const uint32_t nn = static_cast<uint32_t>(hs.nodes.size());
-    DeviceOrder d;
-    d.node_new.assign(nn, 0xFFFFFFFFu);
-    d.group_root.assign(nn, 0);
-    d.node_new[0] = 0;
-    uint32_t pairs = 0;
-    auto place = [&](uint32_t L) {       // the pair (L, L+1) -> the next pair slot
-        d.node_new[L] = 2 * pairs + 1;
-        d.node_new[L + 1] = 2 * pairs + 2;
-        ++pairs;
-    };
-    std::vector<uint32_t> queue;
-    if (nn && hs.nodes[0].axis) queue.push_back(0);
-    for (size_t qi = 0; qi < queue.size(); ++qi) {
-        const uint32_t n = queue[qi];
-        d.group_root[n] = 1;
-        const uint32_t L = hs.nodes[n].left;
-        place(L);
-        for (uint32_t c = L; c <= L + 1; ++c)
-            if (hs.nodes[c].axis) place(hs.nodes[c].left);
-        for (uint32_t c = L; c <= L + 1; ++c)
-            if (hs.nodes[c].axis)
-                for (uint32_t g = hs.nodes[c].left; g <= hs.nodes[c].left + 1; ++g)
-                    if (hs.nodes[g].axis) queue.push_back(g);
-    }
-    d.n_slots = 2 * pairs + 1;
-    // the walk's invariant (descend_steps): a root's inner child has its pair
-    // 1 or 2 pairs after the root's own, the left child's first
-    for (uint32_t n : queue) {
-        const uint32_t L = hs.nodes[n].left, base = d.node_new[L];
-        uint32_t at = base + 2;
-        for (uint32_t c = L; c <= L + 1; ++c)
-            if (hs.nodes[c].axis) {
-                if (d.node_new[hs.nodes[c].left] != at) throw mcpt::Error{MCPT_E_INVALID, "node group layout"};
-                at += 2;
-            }
-    }
-    order_leaves(hs, d);
-    return d;
-}
-
 void build_image(mcpt_scene& s, bool force_global) {
     const mcpt::HostScene& hs = s.hs;
     const uint32_t nt = static_cast<uint32_t>(hs.kd_tris.size());
@@ -388,12 +339,8 @@ void build_image(mcpt_scene& s, bool force_global) {
         boxes = true;
         total = image_size(ord, off_nodes, off_leafs, off_geoms);
     }
-    // 8-B node images: the two-level group order (same size)
-    if (!boxes && MCPT_KD_GROUPS) ord = device_order_groups(hs);
     const size_t off_tris = 0;
     if (total > 0xFFFFFFF0u) throw mcpt::Error{MCPT_E_UNSUPPORTED, "scene image exceeds 4 GiB"};
-    if (!ord.group_root.empty() && ord.n_slots >= (1u << 29))
-        throw mcpt::Error{MCPT_E_UNSUPPORTED, "KD tree too large for grouped node words"};
     if (ord.n_slots >= (1u << 30) || nl >= (1u << 30)) throw mcpt::Error{MCPT_E_UNSUPPORTED, "KD tree too large"};
     s.image.assign(total, 0);
     s.tri_order = ord.tri_order;
@@ -428,7 +375,6 @@ void build_image(mcpt_scene& s, bool force_global) {
         uint32_t w[2];
         if (n.axis) {
             w[0] = ((n.axis - 1u) << 30) | ord.node_new[n.left];
-            if (!ord.group_root.empty() && ord.group_root[i]) w[0] |= 1u << 29;   // trace_device.hpp kGroupBit
             std::memcpy(&w[1], &n.split, 4);
         } else {
             w[0] = (3u << 30) | leaf_begin_new[i];
@@ -560,6 +506,9 @@ Plan make_plan(const mcpt_scene& s, const mcpt_render_params* p) {
     if (p->wf_group_shift != 0 && (p->wf_group_shift < 6 || p->wf_group_shift > 14))
         throw mcpt::Error{MCPT_E_INVALID, "wf_group_shift must be 0 (automatic) or 6..14"};
     if (p->tail_units < 0) throw mcpt::Error{MCPT_E_INVALID, "tail_units must be >= 0"};
+    // (every render path, one device or several, rejects an unknown gather)
+    if (p->gather != MCPT_GATHER_PEER && p->gather != MCPT_GATHER_RCCL)
+        throw mcpt::Error{MCPT_E_INVALID, "unknown gather"};
     const int T = p->tile > 0 ? p->tile : 8;
     if (T > 256) throw mcpt::Error{MCPT_E_INVALID, "tile too large"};
     const int sc = p->shard_count > 1 ? p->shard_count : 1;
@@ -677,10 +626,22 @@ Plan make_plan(const mcpt_scene& s, const mcpt_render_params* p) {
 // wf_mem_limit, or 90% of what the device has free plus what this scene's
 // workspace already holds.  A default batch is halved until every stream's
 // queues fit (never below one pixel's chunk); an explicit batch that does not
-// fit is an error, not a failed hipMalloc half-way through a render.
-void fit_wavefront(const mcpt_scene& s, Plan& pl) {
+// fit is an error, not a failed hipMalloc half-way through a render.  A scene
+// reserved with mcpt_scene_reserve fits a default batch into its reservation
+// (nothing is re-allocated inside a stream capture); if even the smallest
+// batch does not fit there (a reservation made for a smaller render), the
+// render grows the workspace from free memory like an unreserved scene --
+// except on a capturing stream, where that would allocate, so it fails.
+bool stream_capturing(hipStream_t st) {
+    if (!st) return false;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    HIP_TRY(hipStreamIsCapturing(st, &cs));
+    return cs != hipStreamCaptureStatusNone;
+}
+void fit_wavefront(const mcpt_scene& s, Plan& pl, hipStream_t st = nullptr) {
     if (pl.pipeline != MCPT_PIPELINE_WAVEFRONT) return;
     uint64_t budget = pl.wf_mem_limit;
+    bool reserved = false;
     if (!budget) {
         size_t fr = 0, tot = 0;
         HIP_TRY(hipMemGetInfo(&fr, &tot));
@@ -693,13 +654,20 @@ void fit_wavefront(const mcpt_scene& s, Plan& pl) {
                               double(spill > s.ws.spill_bytes ? spill - s.ws.spill_bytes : 0);
         const double avail = (static_cast<double>(fr) + static_cast<double>(s.ws.wf_bytes)) * 0.9 - others;
         budget = avail > 0 ? static_cast<uint64_t>(avail) : 0;
-        // a reserved scene keeps its reservation: a default batch is fitted into it
-        if (s.wf_reserved && !pl.wf_batch_explicit) budget = std::min<uint64_t>(budget, s.wf_reserved);
+        reserved = s.wf_reserved && !pl.wf_batch_explicit;
     }
     auto need = [&](uint64_t cap) { return uint64_t(wf_layout(s, pl, cap).need) * uint64_t(pl.wf_streams); };
-    uint64_t cap = pl.wf_capacity;
-    if (!pl.wf_batch_explicit)
-        while (need(cap) > budget && cap / 2 >= pl.kp.chunk && cap > (uint64_t(1) << 16)) cap /= 2;
+    auto fit = [&](uint64_t b) {
+        uint64_t cap = pl.wf_capacity;
+        if (!pl.wf_batch_explicit)
+            while (need(cap) > b && cap / 2 >= pl.kp.chunk && cap > (uint64_t(1) << 16)) cap /= 2;
+        return cap;
+    };
+    uint64_t cap = fit(reserved ? std::min<uint64_t>(budget, s.wf_reserved) : budget);
+    if (reserved && need(cap) > s.wf_reserved) {
+        if (stream_capturing(st)) budget = std::min<uint64_t>(budget, s.wf_reserved);
+        else cap = fit(budget);
+    }
     if (need(cap) > budget) {
         char msg[256];
         std::snprintf(msg, sizeof msg,
@@ -817,7 +785,7 @@ void render_async(mcpt_scene& s, const mcpt_render_params* p, float* d_fb, hipSt
     }
     set_device(s);
     Plan pl = make_plan(s, p);
-    fit_wavefront(s, pl);
+    fit_wavefront(s, pl, st);
     pl.kp.raw_mean = raw_mean ? 1 : 0;
     // the tail split hands units out by sample, so per-unit counters need whole units
     const int wf_sets = pl.pipeline == MCPT_PIPELINE_WAVEFRONT ? pl.wf_streams : 1;
@@ -930,9 +898,7 @@ uint64_t multi_slot(const Plan& full, const mcpt_render_params* p, int n) {
 void render_multi(mcpt_scene& s, const mcpt_render_params* p, float* d_fb, hipStream_t st) {
     DeviceGuard guard;   // an error on a replica's device must not leave that device current
     set_device(s);
-    const Plan full = make_plan(s, p);                  // validates p; row-major output
-    if (p->gather != MCPT_GATHER_PEER && p->gather != MCPT_GATHER_RCCL)
-        throw mcpt::Error{MCPT_E_INVALID, "unknown gather"};
+    const Plan full = make_plan(s, p);                  // validates p (gather included); row-major output
     const bool use_rccl = p->gather == MCPT_GATHER_RCCL;
     const int n = 1 + static_cast<int>(s.replicas.size());
     const int T = full.kp.tile;

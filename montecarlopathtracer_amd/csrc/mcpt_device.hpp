@@ -42,13 +42,10 @@ __device__ __forceinline__ V3 vdiv(V3 a, float s) { return v3(a.x / s, a.y / s, 
 // midpoint (a - d*m is a multiple of a grid step >= 2^-49 |a| for 24-bit a, d and
 // 25-bit m, and never 0), so the double error cannot change the rounding
 // (tests/test_div_shared.py, tests/test_gpu_math.py).
-//   1: r = IEEE double 1 / d;  2: v_rcp_f64 + two Newton steps (error <= ~2^-52;
-//   0, inf, NaN reciprocals passed through, so a / 0 and a / inf keep IEEE results)
-#ifndef MCPT_SHARED_DIV
-#define MCPT_SHARED_DIV 2
-#endif
+// r = v_rcp_f64 + two Newton steps (error <= ~2^-52; 0, inf, NaN reciprocals
+// passed through, so a / 0 and a / inf keep IEEE results; the IEEE double
+// 1 / d measured 1.9% slower on C2)
 __device__ __forceinline__ double recip_shared(float d) {
-#if MCPT_SHARED_DIV == 2
     const double dd = (double)d;
     const double r0 = __builtin_amdgcn_rcp(dd);
     double e = __builtin_fma(-dd, r0, 1.0);
@@ -56,19 +53,12 @@ __device__ __forceinline__ double recip_shared(float d) {
     e = __builtin_fma(-dd, r1, 1.0);
     const double r2 = __builtin_fma(r1, e, r1);
     return (__builtin_isfinite(r0) && r0 != 0.0) ? r2 : r0;
-#else
-    return 1.0 / (double)d;
-#endif
 }
 __device__ __forceinline__ float div_shared(float a, double r) { return (float)((double)a * r); }
 
 __device__ __forceinline__ void normalize_cu(V3& v) {   // Utils.hpp:27-34
     float len = __builtin_sqrtf(v.x * v.x + v.y * v.y + v.z * v.z);
-#if MCPT_SHARED_DIV
     if (fabsf(len) > kFltEps) { const double r = recip_shared(len); v.x = div_shared(v.x, r); v.y = div_shared(v.y, r); v.z = div_shared(v.z, r); }
-#else
-    if (fabsf(len) > kFltEps) { v.x = v.x / len; v.y = v.y / len; v.z = v.z / len; }
-#endif
 }
 // HLSL normalize(v) = v / length(v) (the D3D definition), no epsilon guard:
 // QuinEngine's shading normal, Fresnel output and primary ray (rtx.hlsl:250,
@@ -76,12 +66,8 @@ __device__ __forceinline__ void normalize_cu(V3& v) {   // Utils.hpp:27-34
 // vector gives NaN like 0 / 0.
 __device__ __forceinline__ void normalize_hlsl(V3& v) {
     const float len = __builtin_sqrtf(v.x * v.x + v.y * v.y + v.z * v.z);
-#if MCPT_SHARED_DIV
     const double r = recip_shared(len);
     v.x = div_shared(v.x, r); v.y = div_shared(v.y, r); v.z = div_shared(v.z, r);
-#else
-    v.x = v.x / len; v.y = v.y / len; v.z = v.z / len;
-#endif
 }
 // __builtin_sqrtf is correctly rounded under HIP defaults; __fsqrt_rn is NOT on gfx950
 // (measured: ~14% of inputs off by 1 ulp, tests/test_gpu_math.py).
@@ -200,52 +186,8 @@ __device__ __forceinline__ float rng_next(uint32_t& sd) {   // rtx.hlsl:74-82
 }
 
 // ------------------------------- samplers -----------------------------------
-// y-up local frame rotated into the normal frame (Utils.hpp:54-68 / :80-93)
-__device__ __forceinline__ V3 sample_hemi(uint32_t& sd, V3 n) {   // Utils.hpp:46-70
-    float x = rng_next(sd);
-    float y = rng_next(sd);
-    float sinT = sqrt_rn(x);
-    float cosT = sqrt_rn(1 - x);
-    float phi = 2 * kPwPi * y;
-    float sp, cp;
-    sincos_f(phi, sp, cp);
-    V3 out = v3(sinT * cp, cosT, sinT * sp);
-    if (fabsf(n.y + 1) < kFltEps) {
-        out = v3(-out.x, -out.y, -out.z);
-    } else if (fabsf(n.y - 1) >= kFltEps) {
-        V3 d = out;
-        float invlen = 1.0f / sqrt_rn(1.0f - n.y * n.y);
-        float len = 1.0f / invlen;
-        out.x = (n.z * d.x + n.x * n.y * d.z) * invlen + n.x * d.y;
-        out.y = n.y * d.y - d.z * len;
-        out.z = (-n.x * d.x + n.z * n.y * d.z) * invlen + n.z * d.y;
-    }
-    return out;
-}
-// Phong lobe; ns1 = the exponent's "Ns + 1" as the caller's type computes it:
-// CVMCTracer passes Ns as unsigned int, (float)(Ns + 1u) (Utils.hpp:72-76);
-// QuinEngine keeps the float, Ns + 1.0f (rtx.hlsl:253-257)
-__device__ __forceinline__ V3 sample_phong(uint32_t& sd, V3 n, V3 in, float ns1) {   // Utils.hpp:72-95
-    float x = rng_next(sd);
-    float y = rng_next(sd);
-    float cosT = pow_f(x, 1.0f / ns1);
-    float sinT = sqrt_rn(1 - cosT * cosT);
-    float phi = 2 * kPwPi * y;
-    float sp, cp;
-    sincos_f(phi, sp, cp);
-    V3 h = v3(sinT * cp, cosT, sinT * sp);
-    if (fabsf(n.y + 1) < kFltEps) {
-        h = v3(-h.x, -h.y, -h.z);
-    } else if (fabsf(n.y - 1) >= kFltEps) {
-        V3 d = h;
-        float invlen = 1.0f / sqrt_rn(1.0f - n.y * n.y);
-        h.x = (n.z * d.x + n.x * n.y * d.z) * invlen + n.x * d.y;
-        h.y = n.y * d.y - d.z / invlen;
-        h.z = (-n.x * d.x + n.z * n.y * d.z) * invlen + n.z * d.y;
-    }
-    return vsub(in, vscale(vscale(h, dot3(in, h)), 2.0f));
-}
-// Diffuse (sample_hemi) and Phong (sample_phong) in one body for a wave that
+// Diffuse (Utils.hpp:46-70 sampleHemi) and Phong (Utils.hpp:72-95) in one
+// body -- the y-up local lobe rotated into the normal frame -- for a wave that
 // holds lanes of both materials: each lane draws its two uniforms and forms
 // (cos, sin) of its own lobe, then the sincos, the lobe vector and the frame
 // rotation -- the bulk of both samplers -- run once for all of them.  Per lane
@@ -253,9 +195,6 @@ __device__ __forceinline__ V3 sample_phong(uint32_t& sd, V3 n, V3 in, float ns1)
 // d.z / invlen for Phong and d.z * (1 / invlen) for the hemisphere.
 // Returns the rotated lobe vector (the hemisphere direction, or Phong's half
 // vector before the reflection).
-#ifndef MCPT_FRESNEL_MERGED
-#define MCPT_FRESNEL_MERGED 1
-#endif
 __device__ __forceinline__ V3 sample_lobe_u(float x, float y, V3 n, bool phong, float ns1) {
     float cosT, sinT;
     if (phong) {
@@ -293,7 +232,6 @@ template <bool QE = false>
 __device__ __forceinline__ V3 sample_fresnel_u(float x, V3 n, V3 in, float Tr, float Ni) {
     float ndoti = dot3(in, n);
     Tr = Tr * (1 - pow5_f(1 - fabsf(ndoti)));
-#if MCPT_FRESNEL_MERGED
     // Entering (ndoti <= 0) and leaving refraction in one body: each lane forms
     // its branch's alpha terms -- the entering branch's six divisions by Ni as
     // RN(a * r) with one shared reciprocal r of Ni (bit-identical to IEEE a / Ni,
@@ -321,27 +259,6 @@ __device__ __forceinline__ V3 sample_fresnel_u(float x, V3 n, V3 in, float Tr, f
     } else {
         out = vsub(in, vscale(vscale(n, dot3(in, n)), 2.0f));
     }
-#else
-    V3 out;
-    if (x < Tr) {
-        if (ndoti <= 0) {
-            float alpha = -ndoti / Ni - sqrt_rn(1 - (1 - ndoti * ndoti) / Ni / Ni);
-            out = vadd(vscale(n, alpha), vdiv(in, Ni));
-            if constexpr (!QE) normalize_cu(out);
-        } else {
-            float test = 1 - (1 - ndoti * ndoti) * Ni * Ni;
-            if (test < 0) {
-                out = vsub(in, vscale(vscale(n, dot3(in, n)), 2.0f));
-            } else {
-                float alpha = -ndoti * Ni + sqrt_rn(test);
-                out = vadd(vscale(n, alpha), vscale(in, Ni));
-                if constexpr (!QE) normalize_cu(out);
-            }
-        }
-    } else {
-        out = vsub(in, vscale(vscale(n, dot3(in, n)), 2.0f));
-    }
-#endif
     if constexpr (QE) normalize_hlsl(out);
     return out;
 }

@@ -25,23 +25,6 @@
 
 namespace mcpt {
 
-// 1: images with 8-B node words (LDS scenes) order their sibling pairs in
-// two-level groups and mark the group roots (bit 29 of an inner node word;
-// trace_device.hpp descend_steps, capi.cpp device_order_groups)
-#ifndef MCPT_KD_GROUPS
-#define MCPT_KD_GROUPS 0
-#endif
-
-// MCPT_WF_HYBRID = 1: the wavefront's LDS scenes run the hybrid extend
-// (wavefront.hip kLayHybrid): node words, leaf refs and geometries in LDS,
-// triangle records (a scene01 image's 41 KB) read through L1/L2, so two
-// 768-thread workgroups with 2-entry stacks fit a CU -- six extend waves per
-// SIMD at <= 80 VGPRs instead of four
-#ifndef MCPT_WF_HYBRID
-#define MCPT_WF_HYBRID 0
-#endif
-constexpr int kHybridBlock = 768, kHybridS = 2, kHybridPerCu = 2;
-
 constexpr int kLdsBlock = 1024;          // in-LDS variant: one 16-wave workgroup per CU
 constexpr int kGlobalBlock = 256;        // global variant
 constexpr int kGlobalBlocksPerCu = 4;

@@ -171,16 +171,10 @@ __device__ __forceinline__ bool tri_prefilter(const RayState& r, const float4 A0
 }
 // the IEEE quotients of the Cramer test (CUTracer.cu:84-92)
 __device__ __forceinline__ void tri_quotients(const TriDets& q, float& beta, float& gamma, float& t) {
-#if MCPT_SHARED_DIV
-    const double rA = recip_shared(q.detA);
+    const double rA = recip_shared(q.detA);   // (= IEEE f32 division, mcpt_device.hpp)
     beta = div_shared(q.qb, rA);
     gamma = div_shared(q.qg, rA);
     t = div_shared(q.qt, rA);
-#else
-    beta = q.qb / q.detA;
-    gamma = q.qg / q.detA;
-    t = q.qt / q.detA;
-#endif
 }
 // the exact tail of a triangle whose prefilter passed
 __device__ __forceinline__ void tri_accept(RayState& r, const TriDets& q, uint32_t prio, uint32_t k) {
@@ -219,9 +213,6 @@ __device__ __forceinline__ void test_tri_v(RayState& r, const float4 A0, const f
 // some lanes passing on a and others on b runs the tail once, not twice.  The
 // closest hit is the lexicographic minimum of (t, rank), so the tail order is
 // immaterial.
-#ifndef MCPT_TAIL_MERGE
-#define MCPT_TAIL_MERGE 1
-#endif
 // EARLY_PRIO (records in global memory): the tail's rank select is made before
 // the tail's branch, so the records' .w words come with their first loads
 // (one 16-B load each) instead of a dependent 4-B load inside the tail
@@ -232,7 +223,6 @@ __device__ __forceinline__ void test_tri_pair(RayState& r, const float4 A0, cons
     TriDets qa, qb;
     const bool oka = tri_prefilter(r, A0, A1, A2, qa);
     const bool okb = tri_prefilter(r, B0, B1, B2, qb) & two;
-#if MCPT_TAIL_MERGE
     uint32_t prio = 0;
     if constexpr (EARLY_PRIO) prio = oka ? __float_as_uint(A0.w) : __float_as_uint(B0.w);
     if (oka | okb) {
@@ -245,10 +235,6 @@ __device__ __forceinline__ void test_tri_pair(RayState& r, const float4 A0, cons
         tri_accept(r, q, prio, oka ? ka : kb);
     }
     if (oka & okb) tri_accept(r, qb, __float_as_uint(B0.w), kb);
-#else
-    if (oka) tri_accept(r, qa, __float_as_uint(A0.w), ka);
-    if (okb) tri_accept(r, qb, __float_as_uint(B0.w), kb);
-#endif
 }
 __device__ __forceinline__ void test_tri(RayState& r, const float4* __restrict__ tris, uint32_t k) {
     test_tri_v(r, tris[k], tris[k + 1], tris[k + 2], k);
@@ -257,14 +243,11 @@ __device__ __forceinline__ void test_tri(RayState& r, const float4* __restrict__
 // A triangle record read whole (16 B): the compiler would narrow reads whose .w
 // is unused to 12 B, and the LDS array serves a ds_read_b96 in 8 cycles, a
 // ds_read_b128 in 4 (MI355X_MICROARCH.md, LDS table).
-#ifndef MCPT_TRI_B128
-#define MCPT_TRI_B128 1
-#endif
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) f32x4 lds_f32x4;
 template <bool IN_LDS>
 __device__ __forceinline__ float4 ld_tri(const float4* __restrict__ p) {
-    if constexpr (IN_LDS && MCPT_TRI_B128) {     // (volatile: not narrowed)
+    if constexpr (IN_LDS) {     // (volatile: not narrowed)
         const f32x4 v = *(const volatile lds_f32x4*)p;
         return make_float4(v.x, v.y, v.z, v.w);
     } else {
@@ -298,15 +281,6 @@ __device__ __forceinline__ float4 ld_tri(const float4* __restrict__ p) {
 #endif
 #ifndef MCPT_DESCENT_CAP_GLOBAL
 #define MCPT_DESCENT_CAP_GLOBAL 5                // global-memory scenes (C4: 5 > 4)
-#endif
-#ifndef MCPT_REC_TAIL8
-#define MCPT_REC_TAIL8 0                         // 1: the pair record's third load is 8 B (global scenes)
-#endif
-#ifndef MCPT_GROUP_LOAD
-#define MCPT_GROUP_LOAD 0                        // 1: a node group's child pairs read by roots only
-#endif
-#ifndef MCPT_GROUP_CAP
-#define MCPT_GROUP_CAP 2                         // node groups: loop iterations of <= 2 levels each
 #endif
 // Child-box cull (scenes in global memory): each sibling-pair record also
 // carries both children's KD boxes (the node region clipped to its
@@ -393,77 +367,12 @@ __device__ __forceinline__ bool pop_entry(RayState& r, uint4* st, int stride, ui
     return !(r.best <= r.tmin * kEpsLo);
 }
 
-// Two-level node groups (scenes whose image has 8-B node words, i.e. LDS
-// scenes; MCPT_KD_GROUPS): the inner nodes at even depth are group roots
-// (kGroupBit in the node word).  A root's sibling pair is followed in the
-// image by the pairs of its inner children -- the left child's first -- so one
-// 48-B read at the root's `left` (three ds_read_b128 issued together) brings
-// both levels below it, and one loop iteration takes two steps of the walk:
-// one LDS round trip and one loop branch per two levels.  The walk, its
-// order, intervals, pushes and counters are the per-level walk's (each level
-// counts as an inner visit); only the device image's pair order changes (the
-// host builds it, capi.cpp device_order_groups).  A popped entry whose node
-// is an odd-depth child (pushed at a group's first level) takes one level,
-// its children are group roots again.
-constexpr uint32_t kGroupBit = 1u << 29;
-constexpr uint32_t kLeftMask = MCPT_KD_GROUPS ? 0x1FFFFFFFu : 0x3FFFFFFFu;   // inner node word: child pair index
-
-// One inner-node step of the ordered walk on 8-B node words: the node in
-// (w0, w1), its children's pair record pr; the far child is pushed when both
-// are needed, (w0, w1) advance to the child entered.
-template <int S, bool COUNT>
-__device__ __forceinline__ void kd_step(RayState& r, uint32_t& w0, uint32_t& w1, const uint4 pr, uint4* st, int stride,
-                                        uint4* __restrict__ spill, uint32_t spill_stride, Counters& c) {
-    const int32_t U = stride * 16;            // one stack position (see slot_of)
-    const int a = (int)(w0 >> 30);
-    const float sv = __uint_as_float(w1);
-    const float oa = sel3(a, r.o.x, r.o.y, r.o.z);
-    const float ia = sel3(a, r.ix, r.iy, r.iz);
-    const float t = (sv - oa) * ia;
-    // near side: below the plane, or on it and heading down; pp = ray inside
-    // the plane (both children).  Only an origin exactly on the plane needs
-    // the direction, so its select and tests sit in a rarely taken branch.
-    bool below = oa < sv, pp = false;
-    if (__builtin_expect(oa == sv, 0)) {
-        const float da = sel3(a, r.d.x, r.d.y, r.d.z);
-        below = da <= 0.0f;
-        pp = da == 0.0f;
-    }
-    // if/else chain of the oracle, evaluated branch-free
-    const float te = t * kEpsHi;
-    const bool no = !(t > 0.0f) | (t > r.tmax);                 // near child only
-    const bool fo = te < r.tmin;                                // far child only
-    const bool go_far = !pp & !no & fo;
-    const bool both = !pp & !no & !fo;                          // push far, go near
-    const bool push_it = pp | both;
-    const uint32_t f0 = below ? pr.z : pr.x, f1 = below ? pr.w : pr.y;     // far child record
-    if (push_it) {
-        // pp ? tmin : max(t, tmin) without the select: a pp lane's t is
-        // (+0) * (+-inf) = NaN (da = +-0, oa == sv), and max returns tmin
-        const float plo = max_qnan(t, r.tmin);
-        lds_uint4* slot = slot_of<S>(st, stride, r.sp);
-        if (r.sp - r.lo == S * U) {       // LDS part full: its oldest entry (same slot) to memory
-            spill[((uint32_t)r.lo / (uint32_t)U) * spill_stride] = ld4(slot);
-            r.lo += U;
-            if constexpr (COUNT) c.spills++;
-        }
-        st4(slot, make_uint4(f0, f1, __float_as_uint(plo), __float_as_uint(r.tmax)));
-        r.sp += U;
-        r.tmax = min_qnan(te, r.tmax);    // here push_it & !pp == both; te = NaN for pp
-    }
-    // the child entered: the near one, or the far one when go_far (the
-    // left record when below != go_far) -- two selects, not four
-    const bool enter_left = below != go_far;
-    w0 = enter_left ? pr.x : pr.z;
-    w1 = enter_left ? pr.y : pr.w;
-}
+constexpr uint32_t kLeftMask = 0x3FFFFFFFu;   // inner node word: child pair index
 
 // Descent of a ray between leaves: at most `cap` inner-node steps (the node
 // record and interval stay in the ray state); 0 = cap reached mid-descent,
 // 1 = a leaf reached (its refs in [lpos, lend)), 2 = the walk ended (a
-// global-memory scene's box cull popped past the last interval).  With node
-// groups (8-B node words, MCPT_KD_GROUPS) `cap` counts loop iterations of up
-// to two levels each.
+// global-memory scene's box cull popped past the last interval).
 // COUNT = false (lean renders): the counters are compiled out.
 template <int S, bool BOXES = false, bool COUNT = true>
 __device__ __forceinline__ int descend_steps(RayState& r, const uint2* __restrict__ nodes1, uint4* st, int stride,
@@ -475,58 +384,18 @@ __device__ __forceinline__ int descend_steps(RayState& r, const uint2* __restric
     uint32_t& w0 = r.nw0;
     uint32_t& w1 = r.nw1;
     int steps = 0;
-    if constexpr (!BOXES && MCPT_KD_GROUPS) {
-        while ((w0 >> 30) != 3u) {
-            if (steps == cap) return 0;       // resume next call
-            steps++;
-            if constexpr (COUNT) c.inner++;
-            MCPT_LANE_USE(desc_w, desc_l, lu);
-            const uint32_t left = w0 & kLeftMask;
-            const bool grp = (w0 & kGroupBit) != 0u;
-            // the node's pair and the two pairs after it (its children's, if it
-            // is a group root), requested together
-            const uint4* g = reinterpret_cast<const uint4*>(nodes1 + left);
-            const uint4 p0 = g[0];
-#if MCPT_GROUP_LOAD
-            uint4 p1 = make_uint4(0, 0, 0, 0), p2 = p1;
-            if (grp) {                        // (only a group root's read brings its children's pairs)
-                p1 = g[1];
-                p2 = g[2];
-            }
-#else
-            const uint4 p1 = g[1], p2 = g[2];
-#endif
-            kd_step<S, COUNT>(r, w0, w1, p0, st, stride, spill, spill_stride, c);
-            if (grp & ((w0 >> 30) != 3u)) {   // a group root's inner child: its pair is in the group
-                if constexpr (COUNT) c.inner++;
-                const uint4 pc = (w0 & kLeftMask) == left + 2u ? p1 : p2;
-                kd_step<S, COUNT>(r, w0, w1, pc, st, stride, spill, spill_stride, c);
-            }
-        }
-        if constexpr (COUNT) c.leaf++;
-        r.lpos = w0 & 0x3FFFFFFFu;
-        r.lend = r.lpos + w1;
-        return 1;
-    }
     while ((w0 >> 30) != 3u) {
         if (steps == cap) return 0;           // resume next call
         steps++;
         if constexpr (COUNT) c.inner++;
         MCPT_LANE_USE(desc_w, desc_l, lu);
-        const uint32_t left = w0 & 0x3FFFFFFFu;
+        const uint32_t left = w0 & kLeftMask;
         uint4 pr, bx0, bx1;
         if constexpr (BOXES) {            // 48-B pair record: words, box(left), box(right)
             const uint4* rec = pairs + 3u * ((left - 1u) >> 1);
             pr = rec[0];
             bx0 = rec[1];
-#if MCPT_REC_TAIL8
-            {   // the record's last 8 B are padding: an 8-B load for the right box's tail
-                const uint2 t = *reinterpret_cast<const uint2*>(rec + 2);
-                bx1 = make_uint4(t.x, t.y, 0u, 0u);
-            }
-#else
             bx1 = rec[2];
-#endif
         } else {
             pr = *reinterpret_cast<const uint4*>(nodes1 + left);   // children left, left+1
         }
@@ -611,9 +480,7 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
     const int32_t U = stride * 16;            // one stack position (see slot_of)
     if (r.lpos == r.lend) {                   // between leaves: descend
         const int k = descend_steps<S, BOXES, COUNT>(r, nodes1, st, stride, spill, spill_stride, c, pairs,
-                                                      CAP > 0 ? CAP : BOXES ? MCPT_DESCENT_CAP_GLOBAL
-                                                                            : (MCPT_KD_GROUPS ? MCPT_GROUP_CAP
-                                                                                              : MCPT_DESCENT_CAP)
+                                                      CAP > 0 ? CAP : BOXES ? MCPT_DESCENT_CAP_GLOBAL : MCPT_DESCENT_CAP
                                                       MCPT_LU_ARG);
         if (k == 0) return false;
         if (k == 2) return true;
@@ -716,9 +583,6 @@ __device__ __forceinline__ V3 emitted(V3 color, const GpuGeom& g, float illum) {
 // n1..n3 are the hit triangle's vertex normals (fetched by the caller).  QE:
 // rtx.hlsl:336-358 -- HLSL normalize of the normal, QE Fresnel (always
 // normalized), Phong with the float Ns; fresnel_kd is 0 for QE (rtx.hlsl:345).
-#ifndef MCPT_MERGED_LOBE
-#define MCPT_MERGED_LOBE 1
-#endif
 template <bool QE = false>
 __device__ __forceinline__ void scatter_n(const GpuGeom& g, float4 n1, float4 n2, float4 n3, float hbeta,
                                           float hgamma, float best, int32_t fresnel_kd, uint32_t& sd, V3& color,
@@ -732,7 +596,6 @@ __device__ __forceinline__ void scatter_n(const GpuGeom& g, float4 n1, float4 n2
         dir = sample_fresnel<QE>(sd, nrm, dir, g.Tr, g.Ni);
         if (fresnel_kd) color = v3(color.x * g.Kd[0], color.y * g.Kd[1], color.z * g.Kd[2]);
     } else {
-#if MCPT_MERGED_LOBE
         // Phong (Utils.hpp:72-95) and diffuse (:46-70) share one sampler body
         const bool ph = g.Ns > 1;
         const bool flip = dot3(dir, nrm) > 0;
@@ -744,18 +607,6 @@ __device__ __forceinline__ void scatter_n(const GpuGeom& g, float4 n1, float4 n2
             color = v3(color.x * g.Kd[0], color.y * g.Kd[1], color.z * g.Kd[2]);
             dir = flip ? v3(-h.x, -h.y, -h.z) : h;
         }
-#else
-        if (g.Ns > 1) {
-            dir = sample_phong(sd, nrm, dir, QE ? g.Ns + 1.0f : (float)(g.Ns_u + 1u));
-            color = v3(color.x * g.Ks[0], color.y * g.Ks[1], color.z * g.Ks[2]);
-        } else {
-            color = v3(color.x * g.Kd[0], color.y * g.Kd[1], color.z * g.Kd[2]);
-            // one inlined sampler for both sides (the flip only negates its result)
-            const bool flip = dot3(dir, nrm) > 0;
-            const V3 hd = sample_hemi(sd, nrm);
-            dir = flip ? v3(-hd.x, -hd.y, -hd.z) : hd;
-        }
-#endif
     }
     // hitPoint = pos + t*dir at the accepted t (CUTracer.cu:89-91), then
     // pos = hitPoint + dir*0.01 (:134,143,159)

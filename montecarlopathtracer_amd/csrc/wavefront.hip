@@ -73,12 +73,10 @@ __device__ __forceinline__ float opaque(float x) {
 __device__ __forceinline__ float4 pack(V3 v, uint32_t w) { return make_float4(v.x, v.y, v.z, __uint_as_float(w)); }
 
 // Queue layout: field k of slot j (kQO {o, pid}, kQD {d, depth}, kQPS
-// {throughput, rng}, kQHIT hit {t, beta, gamma, htri} or the 4-B id).  SoA (default): four float4 streams of
-// slot_stride entries each -- extend's ray reads and hit writes are dense
-// 16-B lane streams; AoS: one 64-B record per slot.
-#ifndef MCPT_WF_SOA
-#define MCPT_WF_SOA 1
-#endif
+// {throughput, rng}, kQHIT hit {t, beta, gamma, htri} or the 4-B id), four
+// SoA float4 streams of slot_stride entries each -- extend's ray reads and hit
+// writes are dense lane streams (64-B AoS records: generate 9 -> 33 ms per C2
+// frame, round 2).
 // WfParams::sort (mcpt_render_params::wf_sort) -- material sort (1): extend
 // appends each finished slot to its segment's class list and shade gathers
 // the records list by list (one material per wave).  Queue order (0, default):
@@ -87,16 +85,11 @@ __device__ __forceinline__ float4 pack(V3 v, uint32_t w) { return make_float4(v.
 // rays to the next queue with one LDS atomic per wave (C2 wavefront 7.56 ->
 // 10.03 G rays/s: the sorted shade's gathers cost more than the divergence).
 __device__ __forceinline__ size_t qf(uint32_t slot, uint32_t k, uint32_t stride) {
-#if MCPT_WF_SOA
     return (size_t)k * stride + slot;
-#else
-    (void)stride;
-    return 4u * (size_t)slot + k;
-#endif
 }
 // queue streams: origin + path id, direction + depth, throughput + RNG state,
-// hit (last: in queue order it holds only 4-B triangle ids, MCPT_WF_HIT_ID, so
-// the queue is 3 x 16 + 4 B per slot; the material sort keeps 16-B hit records)
+// hit (last: in queue order it holds only 4-B triangle ids, so the queue is
+// 3 x 16 + 4 B per slot; the material sort keeps 16-B hit records)
 constexpr uint32_t kQO = 0, kQD = 1, kQPS = 2, kQHIT = 3;
 __device__ __forceinline__ V3 xyz(float4 v) { return v3(v.x, v.y, v.z); }
 
@@ -197,17 +190,12 @@ __device__ __forceinline__ uint32_t seg_queue0_len(const WfParams& wf, uint32_t 
 __host__ __device__ __forceinline__ bool implicit0(const KernelParams& kp, const WfParams& wf) {
     return MCPT_WF_IMPLICIT0 && !wf.sort && kp.mode != kModeQE;
 }
-// MCPT_WF_HIT_ID = 1 (default, queue order): extend writes only the hit
-// triangle's id (4 B, the first quarter of the hit stream as i32) and shade
-// recomputes t, beta, gamma of a scattering ray from it (tri_hit_params: the
-// traversal's own operations, bit-identical).  The 16-B hit records cost the
-// extend 2.4x their bytes in partly written L2 lines; C2 wavefront +3.7%
-// (12.70 -> 13.18, three rounds), C4 +2.8%.
-#ifndef MCPT_WF_HIT_ID
-#define MCPT_WF_HIT_ID 1
-#endif
-static_assert(MCPT_WF_SOA || !MCPT_WF_HIT_ID, "hit ids use the SoA hit stream");
-static_assert(MCPT_WF_HIT_ID && MCPT_WF_SOA, "capi.cpp wf_layout: queue-order queues hold 4-B hit ids, SoA");
+// Hit ids (queue order): extend writes only the hit triangle's id (4 B, the
+// first quarter of the hit stream as i32) and shade recomputes t, beta, gamma
+// of a scattering ray from it (tri_hit_params: the traversal's own
+// operations, bit-identical).  The 16-B hit records cost the extend 2.4x their
+// bytes in partly written L2 lines; C2 wavefront +3.7% (12.70 -> 13.18, three
+// rounds), C4 +2.8%.  (capi.cpp wf_layout sizes the queues for this.)
 
 #if !MCPT_WF_PRIMARY_TU
 // ---- generate: primary rays of the batch (CUTracer.cu:186-211) -------------
@@ -310,19 +298,17 @@ struct ClassBuf {
 #ifndef MCPT_WF_DESCENT_CAP_GLOBAL
 #define MCPT_WF_DESCENT_CAP_GLOBAL MCPT_DESCENT_CAP_GLOBAL
 #endif
-#ifndef MCPT_WF_GROUP_CAP
-#define MCPT_WF_GROUP_CAP 3                      // node groups (LDS scenes): iterations of <= 2 levels
-#endif
-constexpr int kWfLdsCap = MCPT_KD_GROUPS ? MCPT_WF_GROUP_CAP : MCPT_WF_DESCENT_CAP;
+constexpr int kWfLdsCap = MCPT_WF_DESCENT_CAP;
 
 // Residency of the global-memory extend (C4: a walk bound by the latency of
 // node and triangle reads from L2 / MALL, so every resident wave counts).
 // Workgroups of 256 threads, kGlobalBlocksPerCu per CU per launch; other
 // streams' extends fill further slots as far as LDS and VGPRs allow.
-// MCPT_WF_GLOBAL_S: LDS stack entries per lane; MCPT_WF_GLOBAL_MINWG: resident
-// workgroups per CU the compiler must allow (its VGPR budget; the lean
-// queue-order kernel only -- the untimed counting kernels and the material
-// sort's class buffers keep their registers).  6 x 6: 80 VGPRs
+// MCPT_WF_GLOBAL_S: LDS stack entries per lane; MCPT_WF_GLOBAL_WAVES: waves per
+// SIMD the compiler must allow (its VGPR budget; the lean queue-order kernel
+// only -- the untimed counting kernels and the material sort's class buffers
+// keep their registers) -- with 256-thread workgroups (one wave per SIMD
+// each) that is the resident workgroups per CU.  6 x 6: 80 VGPRs
 // (no scratch) and 6 x 24 KB of LDS, six extend waves per SIMD.  C4 G rays/s:
 // S = 8, no hint (round 3: 32 KB, four workgroups, 88 VGPRs) 9.46 / 9.47;
 // S = 6 9.61 / 9.63; S = 7 (five workgroups) 9.85 / 9.87; S = 5 9.20; S = 4
@@ -330,9 +316,10 @@ constexpr int kWfLdsCap = MCPT_KD_GROUPS ? MCPT_WF_GROUP_CAP : MCPT_WF_DESCENT_C
 #ifndef MCPT_WF_GLOBAL_S
 #define MCPT_WF_GLOBAL_S 6
 #endif
-#ifndef MCPT_WF_GLOBAL_MINWG
-#define MCPT_WF_GLOBAL_MINWG 6
+#ifndef MCPT_WF_GLOBAL_WAVES
+#define MCPT_WF_GLOBAL_WAVES 6
 #endif
+static_assert(kGlobalBlock == 256, "MCPT_WF_GLOBAL_WAVES = workgroups per CU only for one wave per SIMD each");
 #ifndef MCPT_WF_GLOBAL_PREFETCH
 #define MCPT_WF_GLOBAL_PREFETCH 1
 #endif
@@ -352,7 +339,7 @@ constexpr int kWfLdsCap = MCPT_KD_GROUPS ? MCPT_WF_GROUP_CAP : MCPT_WF_DESCENT_C
 #define MCPT_WF_GEO_LDS 1
 #endif
 constexpr size_t kLdsPerCu = 160 * 1024;
-constexpr int kLayGlobal = 0, kLayLds = 1, kLayHybrid = 2;
+constexpr int kLayGlobal = 0, kLayLds = 1;
 
 
 #if !MCPT_WF_PRIMARY_TU
@@ -361,16 +348,15 @@ constexpr int kLayGlobal = 0, kLayLds = 1, kLayHybrid = 2;
 // SORT = WfParams::sort, a template argument so that the queue-order variant
 // carries no class-list buffers (8 VGPRs: the co-resident shade of the
 // multi-stream pipeline needs the extend at <= 96)
-// LAY: kLayGlobal (scene image with child-box records in global memory),
-// kLayLds (the whole 8-B-node image copied into LDS), kLayHybrid (node words,
-// leaf refs and geometries in LDS, triangle records read through L1/L2:
-// MCPT_WF_HYBRID, two workgroups per CU)
+// LAY: kLayGlobal (scene image with child-box records in global memory) or
+// kLayLds (the whole 8-B-node image copied into LDS; a hybrid with only the
+// triangle records in L1/L2 and two 768-thread workgroups per CU measured
+// -24%, round 4)
 template <int LAY, int S, int BLOCK, bool COUNT, bool SORT>
-__global__ void __launch_bounds__(BLOCK, (LAY == kLayGlobal && !COUNT && !SORT && MCPT_WF_GLOBAL_MINWG)
-                                             ? MCPT_WF_GLOBAL_MINWG
-                                             : (LAY == kLayHybrid ? 6
-                                                : (LAY == kLayLds && !COUNT && !SORT && MCPT_WF_LDS_WPE
-                                                       ? MCPT_WF_LDS_WPE : 1)))   // (waves per SIMD)
+__global__ void __launch_bounds__(BLOCK, (LAY == kLayGlobal && !COUNT && !SORT && MCPT_WF_GLOBAL_WAVES)
+                                             ? MCPT_WF_GLOBAL_WAVES
+                                             : (LAY == kLayLds && !COUNT && !SORT && MCPT_WF_LDS_WPE
+                                                    ? MCPT_WF_LDS_WPE : 1))   // (waves per SIMD)
 wf_extend(const KernelParams kp, const WfParams wf) {
     constexpr bool IN_LDS = LAY != kLayGlobal;            // node words in LDS
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -383,26 +369,23 @@ wf_extend(const KernelParams kp, const WfParams wf) {
     }
     const int tid = (int)threadIdx.x;
     const GpuScene& sc = kp.scene;
-    // LDS: [stack S x BLOCK x 16 B | scene image (kLayLds) or its part from the
-    // nodes on (kLayHybrid) | 5 counters]
+    // LDS: [stack S x BLOCK x 16 B | scene image (kLayLds) | 5 counters]
     unsigned char* const lds_image = smem + (size_t)S * BLOCK * 16;
-    const uint32_t lds_from = LAY == kLayHybrid ? sc.off_nodes : 0u;   // image offset of lds_image[0]
-    uint32_t* lcnt = reinterpret_cast<uint32_t*>(lds_image + (IN_LDS ? sc.image_bytes - lds_from : 0u));
+    uint32_t* lcnt = reinterpret_cast<uint32_t*>(lds_image + (IN_LDS ? sc.image_bytes : 0u));
     if (tid < 5) lcnt[tid] = 0;
     const float4* tris;
     const uint2* nodes;
     const uint32_t* leafs;
     const GpuGeom* geoms;
     if constexpr (IN_LDS) {
-        const uint4* src = reinterpret_cast<const uint4*>(sc.image + lds_from);
+        const uint4* src = reinterpret_cast<const uint4*>(sc.image);
         uint4* dst = reinterpret_cast<uint4*>(lds_image);
-        const uint32_t n16 = (sc.image_bytes - lds_from) / 16u;
+        const uint32_t n16 = sc.image_bytes / 16u;
         for (uint32_t i = (uint32_t)tid; i < n16; i += BLOCK) dst[i] = src[i];
-        tris = LAY == kLayLds ? reinterpret_cast<const float4*>(lds_image + sc.off_tris)
-                              : reinterpret_cast<const float4*>(sc.image + sc.off_tris);
-        nodes = reinterpret_cast<const uint2*>(lds_image + (sc.off_nodes - lds_from)) + 1;
-        leafs = reinterpret_cast<const uint32_t*>(lds_image + (sc.off_leafs - lds_from));
-        geoms = reinterpret_cast<const GpuGeom*>(lds_image + (sc.off_geoms - lds_from));
+        tris = reinterpret_cast<const float4*>(lds_image + sc.off_tris);
+        nodes = reinterpret_cast<const uint2*>(lds_image + sc.off_nodes) + 1;
+        leafs = reinterpret_cast<const uint32_t*>(lds_image + sc.off_leafs);
+        geoms = reinterpret_cast<const GpuGeom*>(lds_image + sc.off_geoms);
     } else {
         tris = reinterpret_cast<const float4*>(sc.image + sc.off_tris);
         nodes = reinterpret_cast<const uint2*>(sc.image + sc.off_nodes) + 1;
@@ -526,7 +509,7 @@ wf_extend(const KernelParams kp, const WfParams wf) {
                 start(o4, d4);
             }
             if (slot >= count) mode = kDead;
-            if constexpr (MCPT_WF_HIT_ID && !SORT)   // (r holds the next ray by now: the id from hrec)
+            if constexpr (!SORT)   // (r holds the next ray by now: the id from hrec)
                 reinterpret_cast<int32_t*>(qb + qf(0, kQHIT, qs))[seg0 + fslot] = __float_as_int(hrec.w);
             else if constexpr ((MCPT_WF_NT & 4) != 0 || (!IN_LDS && MCPT_WF_NT_HIT_GLOBAL))
                 stq_nt(&qb[qf(seg0 + fslot, kQHIT, qs)], hrec);
@@ -609,10 +592,8 @@ __device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin
 #ifndef MCPT_WF_GEN0
 #define MCPT_WF_GEN0 1
 #endif
-template <int LAY, int S, int BLOCK, bool COUNT>
-__global__ void __launch_bounds__(BLOCK, LAY == kLayHybrid ? 6 : 1) wf_extend_primary(const KernelParams kp,
-                                                                                 const WfParams wf) {
-    static_assert(LAY != kLayGlobal, "the packet walk reads node words from LDS");
+template <int S, int BLOCK, bool COUNT>
+__global__ void __launch_bounds__(BLOCK, 1) wf_extend_primary(const KernelParams kp, const WfParams wf) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t g = blockIdx.x;
     WfCounters* cn = wf.cnt + (size_t)wf.bounce * wf.nseg + g;
@@ -632,21 +613,19 @@ __global__ void __launch_bounds__(BLOCK, LAY == kLayHybrid ? 6 : 1) wf_extend_pr
     const int tid = (int)threadIdx.x;
     const int lane = tid & 63;
     const GpuScene& sc = kp.scene;
-    // LDS: [stack S x BLOCK x 16 B | scene image (from the nodes on: kLayHybrid) | group counter]
+    // LDS: [stack S x BLOCK x 16 B | scene image | group counter]
     unsigned char* const lds_image = smem + (size_t)S * BLOCK * 16;
-    const uint32_t lds_from = LAY == kLayHybrid ? sc.off_nodes : 0u;
-    uint32_t* lgrp = reinterpret_cast<uint32_t*>(lds_image + (sc.image_bytes - lds_from));
+    uint32_t* lgrp = reinterpret_cast<uint32_t*>(lds_image + sc.image_bytes);
     if (tid == 0) *lgrp = 0;
     {
-        const uint4* src = reinterpret_cast<const uint4*>(sc.image + lds_from);
+        const uint4* src = reinterpret_cast<const uint4*>(sc.image);
         uint4* dst = reinterpret_cast<uint4*>(lds_image);
-        const uint32_t n16 = (sc.image_bytes - lds_from) / 16u;
+        const uint32_t n16 = sc.image_bytes / 16u;
         for (uint32_t i = (uint32_t)tid; i < n16; i += BLOCK) dst[i] = src[i];
     }
-    const float4* tris = LAY == kLayLds ? reinterpret_cast<const float4*>(lds_image + sc.off_tris)
-                                        : reinterpret_cast<const float4*>(sc.image + sc.off_tris);
-    const uint2* nodes = reinterpret_cast<const uint2*>(lds_image + (sc.off_nodes - lds_from)) + 1;
-    const uint32_t* leafs = reinterpret_cast<const uint32_t*>(lds_image + (sc.off_leafs - lds_from));
+    const float4* tris = reinterpret_cast<const float4*>(lds_image + sc.off_tris);
+    const uint2* nodes = reinterpret_cast<const uint2*>(lds_image + sc.off_nodes) + 1;
+    const uint32_t* leafs = reinterpret_cast<const uint32_t*>(lds_image + sc.off_leafs);
     __syncthreads();
     uint4* st = reinterpret_cast<uint4*>(smem) + tid;
     uint4* spill = kp.spill + (blockIdx.x * BLOCK + (uint32_t)tid);
@@ -718,8 +697,8 @@ __global__ void __launch_bounds__(BLOCK, LAY == kLayHybrid ? 6 : 1) wf_extend_pr
                 if ((w0 >> 30) != 3u) {
                     // ---- inner node: each lane's step of isect_kd_ordered ----
                     if constexpr (COUNT) c.inner += active ? 1u : 0u;
-                    const uint32_t left = w0 & kLeftMask;     // (one level per node: a group's
-                    const uint4 pr = *reinterpret_cast<const uint4*>(nodes + left);   // first pair)
+                    const uint32_t left = w0 & kLeftMask;
+                    const uint4 pr = *reinterpret_cast<const uint4*>(nodes + left);
                     const int a = (int)(w0 >> 30);
                     const float sv = __uint_as_float(w1);
                     const float oa = sel3(a, eye.x, eye.y, eye.z);   // wave-uniform (common origin)
@@ -799,10 +778,9 @@ __global__ void __launch_bounds__(BLOCK, LAY == kLayHybrid ? 6 : 1) wf_extend_pr
                         const bool two = lend - i >= 2u;
                         const uint32_t k0 = leafs[i], k1n = leafs[i + 1u];
                         const uint32_t k1 = two ? k1n : k0;
-                        constexpr bool TL = LAY == kLayLds;
-                        const float4 a0 = ld_tri<TL>(tris + k0), a1 = ld_tri<TL>(tris + k0 + 1);
-                        const float4 a2 = ld_tri<TL>(tris + k0 + 2), b0 = ld_tri<TL>(tris + k1);
-                        const float4 b1 = ld_tri<TL>(tris + k1 + 1), b2 = ld_tri<TL>(tris + k1 + 2);
+                        const float4 a0 = ld_tri<true>(tris + k0), a1 = ld_tri<true>(tris + k0 + 1);
+                        const float4 a2 = ld_tri<true>(tris + k0 + 2), b0 = ld_tri<true>(tris + k1);
+                        const float4 b1 = ld_tri<true>(tris + k1 + 1), b2 = ld_tri<true>(tris + k1 + 2);
                         if (active) {
                             test_tri_pair(r, a0, a1, a2, k0, b0, b1, b2, k1, two);
                             if constexpr (COUNT) {
@@ -975,13 +953,8 @@ wf_shade_slots(const KernelParams kp, const WfParams wf) {
         V3 o = v3(0, 0, 0), d = v3(0, 0, 0), color = v3(0, 0, 0);
         if (i < total) {
             const size_t js = seg0 + i;
-#if MCPT_WF_HIT_ID
             const int32_t htri = reinterpret_cast<const int32_t*>(qb + qf(0, kQHIT, qs))[js];
             float4 h = make_float4(0, 0, 0, 0);
-#else
-            const float4 h = ldq(&qb[qf(js, kQHIT, qs)]);
-            const int32_t htri = __float_as_int(h.w);
-#endif
             float4 o4, d4, ps;
             if (imp) {   // generate's primary ray, recomputed (a miss or an empty slot needs only pid)
                 pid = slot_pid(wf, g, i);
@@ -1030,9 +1003,7 @@ wf_shade_slots(const KernelParams kp, const WfParams wf) {
                     c.shades++;
                     o = xyz(o4);
                     d = xyz(d4);
-#if MCPT_WF_HIT_ID
                     tri_hit_params(o, d, tris[htri], tris[htri + 1], tris[htri + 2], h.x, h.y, h.z);
-#endif
                     if (qe) scatter<true>(gm, sc.normals, htri, h.y, h.z, h.x, 0, sd, color, o, d);
                     else scatter<false>(gm, sc.normals, htri, h.y, h.z, h.x, kp.fresnel_kd, sd, color, o, d);
                     cont = true;
@@ -1075,9 +1046,9 @@ __global__ void __launch_bounds__(256) wf_accumulate(const KernelParams kp, cons
 
 #endif  // !MCPT_WF_PRIMARY_TU
 
-template <int LAY, int S, int BLOCK>
+template <int S, int BLOCK>
 hipError_t launch_extend_primary(const KernelParams& kp, const WfParams& wf, int grid, size_t lds, hipStream_t st) {
-    auto kern = kp.lean ? wf_extend_primary<LAY, S, BLOCK, false> : wf_extend_primary<LAY, S, BLOCK, true>;
+    auto kern = kp.lean ? wf_extend_primary<S, BLOCK, false> : wf_extend_primary<S, BLOCK, true>;
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
@@ -1113,10 +1084,7 @@ bool wf_in_lds(const GpuScene& sc) { return !sc.node_boxes && lds_bytes_in_lds(s
 // translation unit)
 hipError_t launch_wavefront_primary(const KernelParams& kp, const WfParams& wf, int grid, size_t lds,
                                     hipStream_t st) {
-    if constexpr (MCPT_WF_HYBRID)
-        return launch_extend_primary<kLayHybrid, kHybridS, kHybridBlock>(kp, wf, grid, lds, st);
-    else
-        return launch_extend_primary<kLayLds, 4, kLdsBlock>(kp, wf, grid, lds, st);
+    return launch_extend_primary<4, kLdsBlock>(kp, wf, grid, lds, st);
 }
 #else
 hipError_t launch_wavefront_primary(const KernelParams& kp, const WfParams& wf, int grid, size_t lds,
@@ -1131,12 +1099,11 @@ void read_lane_use_wf(unsigned long long out[6]) {   // wavefront extend lane-us
 #endif
 
 int wavefront_segments(const GpuScene& sc, int cus) {
-    return wf_in_lds(sc) ? (MCPT_WF_HYBRID ? kHybridPerCu * cus : cus) : cus * kWfGlobalSegsPerCu;
+    return wf_in_lds(sc) ? cus : cus * kWfGlobalSegsPerCu;
 }
 // LDS bytes of an LDS-scene extend workgroup: stack + image (or its part from the nodes on) + counters
 size_t wf_lds_extend_bytes(const GpuScene& sc) {
-    return MCPT_WF_HYBRID ? (size_t)kHybridS * kHybridBlock * 16 + (sc.image_bytes - sc.off_nodes) + 32
-                          : lds_bytes_in_lds(sc.image_bytes, 4) + 32;
+    return lds_bytes_in_lds(sc.image_bytes, 4) + 32;
 }
 
 hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams* wf_in, const WfStreams& ws, int cus,
@@ -1199,7 +1166,7 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams* wf_in, co
             const uint32_t n = wf.nb * wf.ns;
             // the shade's material table in LDS if it fits beside the extend's
             // workgroups on a CU (MCPT_WF_GEO_LDS)
-            const size_t ext_lds = in_lds ? (MCPT_WF_HYBRID ? kHybridPerCu : 1) * wf_lds_extend_bytes(kp.scene)
+            const size_t ext_lds = in_lds ? wf_lds_extend_bytes(kp.scene)
                                           : (size_t)kWfGlobalSegsPerCu * (MCPT_WF_GLOBAL_S * kGlobalBlock * 16 + 32);
             const size_t geo_bytes = (MCPT_WF_GEO_LDS && ext_lds + 64 * (size_t)kp.scene.n_geoms + 64 <= kLdsPerCu)
                                          ? 64 * (size_t)kp.scene.n_geoms : 0;
@@ -1214,8 +1181,8 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams* wf_in, co
             // bounce 0 of CV mode (implicit queue 0: every origin is the eye): the
             // wave-coherent extend, one tree walk per 64-ray tile (MCPT_WF_PACKET0),
             // which also generates the primary rays (MCPT_WF_GEN0)
-            // (the packet extend stores hit ids only: it needs MCPT_WF_HIT_ID's shade)
-            const bool packet = MCPT_WF_PACKET0 && MCPT_WF_HIT_ID && in_lds && MCPT_WF_IMPLICIT0 >= 2 &&
+            // (the packet extend stores hit ids only: it needs the queue-order shade)
+            const bool packet = MCPT_WF_PACKET0 && in_lds && MCPT_WF_IMPLICIT0 >= 2 &&
                                 implicit0(kb, wf) && wf.group_shift == 6u;
             if (!(packet && MCPT_WF_GEN0)) {
                 const uint32_t gen_grid = (n + kGenBlock - 1) / kGenBlock;
@@ -1229,10 +1196,7 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams* wf_in, co
                 if (packet && b == 0) {
                     e = launch_wavefront_primary(kb, wf, (int)nseg, llds, bs);
                 } else if (in_lds) {
-                    if constexpr (MCPT_WF_HYBRID)
-                        e = launch_extend<kLayHybrid, kHybridS, kHybridBlock>(kb, wf, (int)nseg, llds, bs);
-                    else
-                        e = launch_extend<kLayLds, 4, kLdsBlock>(kb, wf, (int)nseg, llds, bs);
+                    e = launch_extend<kLayLds, 4, kLdsBlock>(kb, wf, (int)nseg, llds, bs);
                 } else
                     e = launch_extend<kLayGlobal, MCPT_WF_GLOBAL_S, kGlobalBlock>(kb, wf, (int)nseg,
                                                                             (size_t)MCPT_WF_GLOBAL_S * kGlobalBlock * 16 + 32,

@@ -12,7 +12,7 @@ fi
 alt="--no-alt"; [ -z "$NOALT" ] && alt=""
 for round in $(seq 1 ${ROUNDS:-2}); do
 for lib in $LIBS; do
-  MCPT_LIB_PATH=$PWD/montecarlopathtracer_amd/lib/$lib timeout -k 10 300 python bench.py $alt --steps ${STEPS:-5} --warmup 1 --no-cpu-baseline --no-pmc $ARGS > gpurun_out/ab2/b_${lib}_$round.log 2>&1
+  MCPT_LIB_PATH=$PWD/montecarlopathtracer_amd/lib/$lib timeout -k 10 300 python bench.py $alt --steps ${STEPS:-5} --warmup 1 --no-cpu-baseline --no-pmc --no-c5 $ARGS > gpurun_out/ab2/b_${lib}_$round.log 2>&1
   python3 - gpurun_out/ab2/b_${lib}_$round.log "$round $lib" <<'PY'
 import json, sys
 ln = [json.loads(x) for x in open(sys.argv[1]) if x.startswith("{")][-1]

@@ -11,7 +11,7 @@ if [ -z "$NOTEST" ]; then
 fi
 for round in $(seq 1 ${ROUNDS:-2}); do
 for lib in $LIBS; do
-  MCPT_LIB_PATH=$PWD/montecarlopathtracer_amd/lib/$lib timeout -k 10 300 python bench.py --no-alt --steps ${STEPS:-5} --warmup 1 --no-cpu-baseline --no-pmc $ARGS > gpurun_out/ab/b_$lib.log 2>&1
+  MCPT_LIB_PATH=$PWD/montecarlopathtracer_amd/lib/$lib timeout -k 10 300 python bench.py --no-alt --steps ${STEPS:-5} --warmup 1 --no-cpu-baseline --no-pmc --no-c5 $ARGS > gpurun_out/ab/b_$lib.log 2>&1
   echo "round $round $lib: $(grep -o '"value": [0-9.]*' gpurun_out/ab/b_$lib.log | head -1) $(grep -o '"kernel_ms_avg": [0-9.]*' gpurun_out/ab/b_$lib.log)"
 done
 done

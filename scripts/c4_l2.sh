@@ -10,7 +10,7 @@ for lib in $LIBS; do
   O=$R/gpurun_out/c4_l2/$lib
   rm -rf $O; mkdir -p $O
   (cd /tmp && MCPT_LIB_PATH=$R/montecarlopathtracer_amd/lib/$lib timeout -k 10 240 rocprofv3 --pmc TCC_HIT TCC_MISS \
-     --output-format csv -d $O -o run -- python3 $R/bench.py --scene cornell_bunny70k --no-alt --no-pmc --no-c4 \
+     --output-format csv -d $O -o run -- python3 $R/bench.py --scene cornell_bunny70k --no-alt --no-pmc --no-extra \
      --no-cpu-baseline --steps 1 --warmup 0 $ARGS > $O/log 2>&1)
   python3 - $O $lib <<'PY'
 import importlib.util, os, sys

@@ -6,6 +6,6 @@
 set -e
 mkdir -p gpurun_out/phase
 for lib in $LIBS; do
-  MCPT_LIB_PATH=$PWD/montecarlopathtracer_amd/lib/$lib timeout -k 10 300 python bench.py --no-alt --no-pmc --no-cpu-baseline --no-c4 --steps 1 --warmup 0 --wf-streams 1 $ARGS > gpurun_out/phase/$lib.log 2>&1
+  MCPT_LIB_PATH=$PWD/montecarlopathtracer_amd/lib/$lib timeout -k 10 300 python bench.py --no-alt --no-pmc --no-cpu-baseline --no-extra --steps 1 --warmup 0 --wf-streams 1 $ARGS > gpurun_out/phase/$lib.log 2>&1
   echo "$lib: $(grep -h 'lane use' gpurun_out/phase/$lib.log | tail -1)"
 done

@@ -4,7 +4,7 @@
 set -e
 mkdir -p gpurun_out/sweep
 for v in $VALUES; do
-  timeout -k 10 300 python bench.py --no-alt --no-pmc --no-cpu-baseline --no-c4 --steps ${STEPS:-5} --warmup 1 --set $FIELD=$v $ARGS > gpurun_out/sweep/${FIELD}_$v.log 2>&1
+  timeout -k 10 300 python bench.py --no-alt --no-pmc --no-cpu-baseline --no-extra --steps ${STEPS:-5} --warmup 1 --set $FIELD=$v $ARGS > gpurun_out/sweep/${FIELD}_$v.log 2>&1
   python3 - gpurun_out/sweep/${FIELD}_$v.log "$FIELD=$v" <<'PY'
 import json, sys
 ln = [json.loads(x) for x in open(sys.argv[1]) if x.startswith("{")][-1]

@@ -289,3 +289,58 @@ def test_pw_tracer_dropin_rccl_gather(mcpt, tmp_path):
     host = np.zeros((30, 40, 3), np.float32)
     tr.render_scene(1, host, num_kernels=3, samples_per_kernel=4)
     assert np.array_equal(got, host)
+
+
+def test_small_reservation_then_larger_render(mcpt):
+    """A scene reserved for a small wavefront render (work below one minimum
+    batch) still renders a larger one later: the default batch that does not
+    fit the reservation grows the workspace from free memory (capi.cpp
+    fit_wavefront; only a capturing stream is held to the reservation)."""
+    kw = dict(width=96, height=64, spp=64, spp_chunk=8, pipeline="wavefront")
+    ref, rs = mcpt.Scene(mcpt.ObjModel(mcpt.scene_path("scene01"))).render(mcpt.RenderParams(**kw))
+    scene = mcpt.Scene(mcpt.ObjModel(mcpt.scene_path("scene01")))
+    fresh_plan = scene.plan(mcpt.RenderParams(**kw))
+    scene.reserve(mcpt.RenderParams(width=16, height=16, spp=2, spp_chunk=2, pipeline="wavefront"))
+    assert scene.plan(mcpt.RenderParams(**kw))["wf_batch"] == fresh_plan["wf_batch"]
+    img, st = scene.render(mcpt.RenderParams(**kw))
+    assert np.array_equal(img, ref) and st["rays"] == rs["rays"]
+
+
+@pytest.mark.parametrize("n", [1, 2])
+def test_unknown_gather_rejected_on_every_path(mcpt, devices, n):
+    """mcpt_render_params::gather other than PEER / RCCL is MCPT_E_INVALID on a
+    one-device scene too, not only where a multi-device render reads it."""
+    import ctypes as C
+    from montecarlopathtracer_amd._capi import RenderStats, lib
+    devices([0] * n)
+    scene = mcpt.Scene(mcpt.ObjModel(mcpt.scene_path("scene01")))
+    p = mcpt.RenderParams(width=16, height=16, spp=1).to_c()
+    p.gather = 2
+    fb = np.zeros((16, 16, 3), np.float32)
+    st = RenderStats()
+    rc = lib().mcpt_render(scene.handle, C.byref(p), fb.ctypes.data_as(C.POINTER(C.c_float)), C.byref(st))
+    assert rc == -1, rc   # MCPT_E_INVALID
+    assert b"unknown gather" in lib().mcpt_last_error()
+
+
+def _distinct_gpus():
+    try:
+        import torch
+        return torch.cuda.device_count()
+    except Exception:
+        return 0
+
+
+@pytest.mark.skipif(_distinct_gpus() < 2, reason="needs two distinct GPUs (the RCCL gather across devices)")
+@pytest.mark.parametrize("pipeline", ["megakernel", "wavefront"])
+def test_rccl_gather_two_devices_equals_peer(mcpt, devices, pipeline):
+    """The grouped ncclGather across distinct devices (capi.cpp render_multi:
+    rank streams, slot-sized send buffers, done events after ncclGroupEnd)
+    lands the same image as the peer-copy gather, bit for bit."""
+    devices([0, 1])
+    scene = mcpt.Scene(mcpt.ObjModel(mcpt.scene_path("scene01")))
+    kw = dict(width=67, height=45, spp=5, spp_chunk=2, pipeline=pipeline)
+    peer, sp = scene.render(mcpt.RenderParams(gather="peer", **kw))
+    rccl, sr = scene.render(mcpt.RenderParams(gather="rccl", **kw))
+    assert np.array_equal(rccl.view(np.uint32), peer.view(np.uint32))
+    assert sr["rays"] == sp["rays"] and sr["devices"] == 2

@@ -1,8 +1,8 @@
 """The N > 1 paths on the GPU, as the driver's multi-GPU runs will first execute
 them (BASELINE configs[2]: pixel tiles across ranks + a tile gather to rank 0).
 
-* bench.py's rank path with world_size 2 (torch.distributed.run, gloo, both
-  ranks on GPU 0): rank 0's gathered image equals the single-GPU render bit
+* bench.py's rank path with world_size 2 and 8 (torch.distributed.run, gloo,
+  every rank on GPU 0): rank 0's gathered image equals the single-GPU render bit
   for bit, and the JSON line carries n_gpus == 2 and the roofline of rank 0's
   shard.  RCCL itself needs two distinct GPUs (a communicator refuses a
   repeated device), so the driver's 8-GPU node is where "nccl" first runs;
@@ -38,9 +38,9 @@ def _free_port():
     return port
 
 
-def _single_gpu_image(mcpt, pipeline="wavefront"):
+def _single_gpu_image(mcpt, pipeline="wavefront", w=W, h=H):
     scene = mcpt.Scene(mcpt.ObjModel(mcpt.scene_path("scene01")))
-    img, st = scene.render(mcpt.RenderParams(width=W, height=H, spp=SPP, spp_chunk=32, pipeline=pipeline))
+    img, st = scene.render(mcpt.RenderParams(width=w, height=h, spp=SPP, spp_chunk=32, pipeline=pipeline))
     return img, st
 
 
@@ -50,24 +50,31 @@ def _bench_line(stdout: str) -> dict:
     return json.loads(lines[0])
 
 
-def test_bench_rank_path_world2_gloo(mcpt, tmp_path):
+# world 8: the driver's N = 8 dealing with an uneven tile split (33 x 25 tiles
+# of 8 x 8 = 825 over 8 ranks: 104 for rank 0, 103 for the others, so
+# TileGather pads to the largest shard), all eight ranks on GPU 0; rank 0's
+# PMC passes only at world 2 (the roofline plumbing), not repeated at 8
+@pytest.mark.parametrize("world,w,h,pmc", [(2, W, H, True), (8, 264, 200, False)])
+def test_bench_rank_path_gloo(mcpt, tmp_path, world, w, h, pmc):
     out = str(tmp_path / "img.npy")
     env = dict(os.environ, MCPT_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--width", str(W), "--height", str(H), "--spp", str(SPP),
-           "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--dump-image", out]
+           os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--width", str(w), "--height", str(h),
+           "--spp", str(SPP), "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--dump-image", out]
+    if not pmc:
+        cmd.append("--no-pmc")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=280, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     line = _bench_line(r.stdout)
-    assert line["n_gpus"] == 2 and line["value"] > 0
+    assert line["n_gpus"] == world and line["value"] > 0
     assert "gloo gather" in line["config"]["parallelism"]
     roof = line["roofline"]
     assert roof["bound"] == "hbm" and roof["peak"] > 0 and "source" in roof
-    if roof["achieved"] is not None:              # rocprofv3 present: rank 0's shard measured
+    if pmc and roof["achieved"] is not None:      # rocprofv3 present: rank 0's shard measured
         assert roof["frac"] > 0 and "rank 0's shard" in roof["source"]
     got = np.load(out)
-    ref, st = _single_gpu_image(mcpt)
+    ref, st = _single_gpu_image(mcpt, w=w, h=h)
     assert np.array_equal(got[..., :3], ref)
     # whole-job rays: both ranks' shards = the single-GPU frame's rays per step
     assert line["rays_per_step"] == st["rays"]
@@ -95,7 +102,7 @@ def _worker(rank, world, port, pipeline, out_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 @pytest.mark.parametrize("pipeline", ["wavefront", "megakernel"])
 def test_gpu_rendered_shards_gather_gloo(mcpt, tmp_path, world, pipeline):
     out = str(tmp_path / "img.npy")
