@@ -28,9 +28,9 @@ def kernel_text(lib):
             cur = None
             for line in txt.splitlines():
                 m = re.match(r"^(\S+):$", line.strip()) if line and not line.startswith((" ", "\t")) else None
-                if m or re.match(r"^[0-9a-f]* ?<(\S+)>:$", line.strip()):
-                    name = (m.group(1) if m else re.match(r"^[0-9a-f]* ?<(\S+)>:$", line.strip()).group(1))
-                    cur = name
+                if m or re.match(r"^[0-9a-f]* ?<?(\S+?)>?:$", line.strip()):
+                    name = (m.group(1) if m else re.match(r"^[0-9a-f]* ?<?(\S+?)>?:$", line.strip()).group(1))
+                    cur = name.strip("<>")
                     out.setdefault(cur, [])
                     continue
                 if cur and line.strip():
