@@ -160,6 +160,10 @@ def wavefront_hbm(args, shard=(1, 0)) -> dict:
                         "GRBM_GUI_ACTIVE"], "wf_valu", reader=read_wf_kernels, shard=shard)
     ld = pmc_pass(args, ["SQ_INSTS_LDS", "SQ_LDS_IDX_ACTIVE", "SQ_LDS_BANK_CONFLICT", "GRBM_GUI_ACTIVE"], "wf_lds",
                   reader=read_wf_kernels, shard=shard)
+    # the L2's fabric read requests by size (FETCH_SIZE's inputs on gfx950): exact bytes
+    # = 32 n32 + 64 n64 + 128 n128, the calibration of FETCH_SIZE x 2 for this access pattern
+    rq = pmc_pass(args, ["TCC_EA0_RDREQ", "TCC_EA0_RDREQ_32B", "TCC_EA0_RDREQ_64B", "TCC_EA0_RDREQ_128B"], "wf_req",
+                  reader=read_wf_kernels, shard=shard)
     res = {}
     for cls in f:
         if cls not in w or "FETCH_SIZE" not in f[cls] or "WRITE_SIZE" not in w[cls]:
@@ -175,6 +179,14 @@ def wavefront_hbm(args, shard=(1, 0)) -> dict:
         if cls in ld:
             res[cls]["lds_counters"] = {k: ld[cls][k] for k in ld[cls] if k.startswith(("SQ_", "GRBM_"))}
             res[cls]["lds_counters"]["ns"] = ld[cls]["ns"]
+        if cls in rq and "TCC_EA0_RDREQ_128B" in rq[cls]:
+            q = rq[cls]
+            exact = 32.0 * q.get("TCC_EA0_RDREQ_32B", 0) + 64.0 * q.get("TCC_EA0_RDREQ_64B", 0) + \
+                128.0 * q["TCC_EA0_RDREQ_128B"]
+            res[cls]["read_requests"] = {"n32": q.get("TCC_EA0_RDREQ_32B"), "n64": q.get("TCC_EA0_RDREQ_64B"),
+                                         "n128": q["TCC_EA0_RDREQ_128B"], "all": q.get("TCC_EA0_RDREQ"),
+                                         "exact_read_GB": round(exact / 1e9, 3),
+                                         "fetch_size_factor": round(exact / (f[cls]["FETCH_SIZE"] * 1024.0), 4)}
     return res
 
 
@@ -603,6 +615,21 @@ def main():
                             launches=ext["launches"], kernel_ms=ext["ms"],
                             avg_launch_ms=round(ext["ms"] / max(ext["launches"], 1), 4),
                             timing="sum of the extend dispatches' durations in the PMC pass (kernels serialized)")
+                rr = ext.get("read_requests")
+                if rr:
+                    # the extend's ray stream (bounce 0 reads 16 B per path: the direction, the origin is the
+                    # eye; later bounces 32 B: origin + direction) against the exact fabric reads: the rest
+                    # is node / triangle records (and stack refills) fetched past the L2
+                    shard_rays, shard_paths = per_launch["rays"] / n_gpus, per_launch["paths"] / n_gpus
+                    ray_gb = (16.0 * shard_paths + 32.0 * (shard_rays - shard_paths)) / 1e9
+                    roof["read_split"] = {
+                        "exact_read_GB": rr["exact_read_GB"], "fetch_size_factor": rr["fetch_size_factor"],
+                        "ray_GB": round(ray_gb, 3), "record_GB": round(rr["exact_read_GB"] - ray_gb, 3),
+                        "hit_id_write_GB": round(4.0 * shard_rays / 1e9, 3),
+                        "spill_write_GB": round(16.0 * per_launch["stack_spills"] / n_gpus / 1e9, 3),
+                        "method": "TCC_EA0_RDREQ_{32B,64B,128B} pass: exact = 32 n32 + 64 n64 + 128 n128 (every "
+                                  "request 128 B here; FETCH_SIZE counts 64 B each, factor 2 exactly, "
+                                  "scripts/fetch_calib.hip); ray_GB from the counted rays / paths"}
                 vb = valu_block(ext.pop("valu_counters", {}), cus, ext.get("ms", 0.0), per_launch["rays"] / n_gpus)
                 if vb:
                     vb["kernel"] = "wf_extend (the traversal: the dominant kernel), run alone"

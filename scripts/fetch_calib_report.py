@@ -19,9 +19,9 @@ import sys
 
 KNOWN = {   # kernel -> (label, known bytes given the records count n)
     "calib_stream": ("stream 1 GiB, 16 B/lane", lambda n: 1 << 30),
-    "calib_gatherILi128ELi0E": ("48-B records, one per 128-B line, offset 0", lambda n: 4 * n + 48 * n),
-    "calib_gatherILi128ELi40E": ("48-B records, one per 128-B line, offset 40", lambda n: 4 * n + 48 * n),
-    "calib_gatherILi48ELi0E": ("packed 48-B records (C4 pair-record layout)", lambda n: 4 * n + 48 * n),
+    "calib_gather<128, 0>": ("48-B records, one per 128-B line, offset 0", lambda n: 4 * n + 48 * n),
+    "calib_gather<128, 40>": ("48-B records, one per 128-B line, offset 40", lambda n: 4 * n + 48 * n),
+    "calib_gather<48, 0>": ("packed 48-B records (C4 pair-record layout)", lambda n: 4 * n + 48 * n),
 }
 
 
@@ -94,8 +94,11 @@ def main(d, c4line=None):
         out = {k[:-2] + "_GB": v for k, v in out.items()}
         if "fetch_size_B" in c4 and "read_exact_B" in c4:
             out["exact_over_fetch_size"] = round(c4["read_exact_B"] / c4["fetch_size_B"], 4)
+        out["requests"] = c4.get("requests")
+        out["write_counters"] = {k: v for k, v in c4["counters"].items() if "WR" in k}
         if c4line and os.path.exists(c4line):
             ln = [json.loads(x) for x in open(c4line) if x.startswith("{")][-1]
+            ln = (ln.get("extra_lines") or {}).get("c4", ln)   # the C4 line of a default bench line
             rays, paths = ln["rays_per_step"], ln["paths_per_step"]
             # the extend's ray stream: bounce 0 reads 16 B (direction; the origin is the eye), later
             # bounces 32 B (origin + direction); it writes a 4-B hit id per ray

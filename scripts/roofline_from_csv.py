@@ -6,7 +6,10 @@ summed duration in the FETCH_SIZE pass, frac = achieved / 8000 GB/s; with the
 bench line (its per-ray counts, rays per frame and the CU count it ran on) also
 roofline.lds from the wf_lds pass and roofline.binding_frac (max of the HBM,
 LDS-array and VALU-issue fractions; the VALU figure from the wf_valu pass).
-usage: roofline_from_csv.py profiles/r04/pmc_wf [profiles/r04/bench.jsonl] [CUs=256]"""
+With a wf_req pass (TCC_EA0_RDREQ by request size) also the exact fabric read
+bytes, FETCH_SIZE's factor for this pattern, and the ray-stream / record split.
+usage: roofline_from_csv.py profiles/r05/pmc_wf [profiles/r05/bench.jsonl] [CUs=256] [c4|c5]
+       (c4 / c5: the bench line's extra line of that name, with DIR its pmc_wf/c4 csv)"""
 import importlib.util
 import json
 import os
@@ -15,7 +18,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def main(d, line=None, cus=256):
+def main(d, line=None, cus=256, extra=None):
     spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
     b = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(b)
@@ -25,10 +28,25 @@ def main(d, line=None, cus=256):
     gbs = (rd + wr) / f["ns"]
     out = {"extend_read_GB": round(rd / 1e9, 3), "extend_write_GB": round(wr / 1e9, 3), "ms": round(f["ns"] / 1e6, 3),
            "launches": f["dispatches"], "achieved_GBps": round(gbs, 2), "frac": round(gbs / b.HBM_PEAK_GBS, 5)}
+    qd = os.path.join(d, "wf_req")
+    if os.path.isdir(qd):   # exact fabric reads by request size (the FETCH_SIZE calibration)
+        q = b.read_wf_kernels(qd)["extend"]
+        exact = 32.0 * q.get("TCC_EA0_RDREQ_32B", 0) + 64.0 * q.get("TCC_EA0_RDREQ_64B", 0) + \
+            128.0 * q["TCC_EA0_RDREQ_128B"]
+        out["exact_read_GB"] = round(exact / 1e9, 3)
+        out["fetch_size_factor"] = round(exact / (f["FETCH_SIZE"] * 1024.0), 4)
     if line:
         ln = [json.loads(x) for x in open(line) if x.startswith("{")][-1]
+        if extra:   # e.g. c4: the line's extra line of that name
+            ln = ln["extra_lines"][extra]
         r = ln["roofline"]
-        out["bench_line"] = {"achieved": r["achieved"], "frac": r["frac"], "traffic": r["traffic"]}
+        if "exact_read_GB" in out:
+            rays = ln["rays_per_step"] / ln["n_gpus"]
+            paths = ln["paths_per_step"] / ln["n_gpus"]
+            ray_gb = (16.0 * paths + 32.0 * (rays - paths)) / 1e9
+            out["ray_GB"], out["record_GB"] = round(ray_gb, 3), round(out["exact_read_GB"] - ray_gb, 3)
+        out["bench_line"] = {"achieved": r["achieved"], "frac": r["frac"], "traffic": r["traffic"],
+                             "read_split": r.get("read_split")}
         cus = int(cus)
         roof = {"frac": out["frac"]}
         vd = os.path.join(d, "wf_valu")
