@@ -392,7 +392,8 @@ wf_extend(const KernelParams kp, const WfParams wf) {
         leafs = reinterpret_cast<const uint32_t*>(sc.image + sc.off_leafs);
         geoms = reinterpret_cast<const GpuGeom*>(sc.image + sc.off_geoms);
     }
-    const uint4* pairs = reinterpret_cast<const uint4*>(sc.image + sc.off_nodes);   // 48-B pair records (global variant)
+    const uint4* pairs = reinterpret_cast<const uint4*>(sc.image + sc.off_nodes);   // 32-B pair records (global variant)
+    const BoxGridD bg = box_grid_of(sc);
     __syncthreads();
     uint4* st = reinterpret_cast<uint4*>(smem) + tid;
     uint4* spill = kp.spill + (blockIdx.x * BLOCK + (uint32_t)tid);
@@ -461,7 +462,7 @@ wf_extend(const KernelParams kp, const WfParams wf) {
 #endif
             if (mode == kTrav) {
                 if (trav_iter<S, !IN_LDS, COUNT, LAY == kLayLds, IN_LDS ? kWfLdsCap : MCPT_WF_DESCENT_CAP_GLOBAL>(r, tris, nodes, leafs, st, BLOCK, spill, spill_stride, c MCPT_LU_ARG,
-                                                 pairs))
+                                                 pairs, bg))
                     mode = kReady;
             }
             const uint64_t trv = __ballot(mode == kTrav);
