@@ -713,7 +713,9 @@ struct SlotCursor {
 
 // counters: wave reduction in 64 bits (64 lanes of 32-bit counts may exceed
 // 2^32), one atomic per wave per counter
-__device__ __forceinline__ void flush_counters(const Counters& c, unsigned long long* stats) {
+__device__ __forceinline__ void flush_counters(const Counters& c, unsigned long long* stats,
+                                               uint32_t lane = ~0u) {   // (lane: this lane's index, if at hand)
+    if (lane == ~0u) lane = threadIdx.x & 63u;
     const uint32_t vals[8] = {c.rays, c.paths, c.inner, c.leaf, c.refs, c.tests, c.shades, c.spills};
     unsigned long long sums[8];
 #pragma unroll
@@ -723,7 +725,7 @@ __device__ __forceinline__ void flush_counters(const Counters& c, unsigned long 
         for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
         sums[i] = x;
     }
-    if ((threadIdx.x & 63u) == 0) {
+    if (lane == 0) {
 #pragma unroll
         for (int i = 0; i < 8; i++)
             if (sums[i]) atomicAdd(stats + i, sums[i]);
