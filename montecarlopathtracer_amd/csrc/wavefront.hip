@@ -409,13 +409,15 @@ struct HitCombiner {
     }
     // every lane: count the ids put (a, b of the lanes whose ray ended) and store every
     // complete reservation with one coalesced wave store
-    __device__ __forceinline__ void commit(bool a, bool b, int32_t* hq, uint32_t lane) {
+    __device__ __forceinline__ void commit(bool a, bool b, uint32_t count, int32_t* hq, uint32_t lane) {
         const uint32_t r0 = (s0 & 127u) - (uint32_t)__popcll(__ballot(a));
         const uint32_t r1 = (s1 & 127u) - (uint32_t)__popcll(__ballot(b));
         const bool f0 = (chunk(s0) != kFree) & (r0 == 0u), f1 = (chunk(s1) != kFree) & (r1 == 0u);
-        // (a complete buffer holds every slot of its reservation below the queue length)
-        if (f0 && lane < (s0 & 127u)) hq[chunk(s0) * kChunk + lane] = (int32_t)buf[lane];
-        if (f1 && lane < (s1 & 127u)) hq[chunk(s1) * kChunk + lane] = (int32_t)buf[kChunk + lane];
+        // a complete buffer holds every slot of its reservation below the queue length
+        const uint32_t cnt = rfl(count);
+        const uint32_t v0 = cnt - chunk(s0) * kChunk, v1 = cnt - chunk(s1) * kChunk;   // (>= 1 when in use)
+        if (f0 && lane < v0) hq[chunk(s0) * kChunk + lane] = (int32_t)buf[lane];
+        if (f1 && lane < v1) hq[chunk(s1) * kChunk + lane] = (int32_t)buf[kChunk + lane];
         s0 = rfl(f0 ? (kFree << 7) : ((s0 & ~127u) | r0));
         s1 = rfl(f1 ? ((s1 & 0x80000000u) | (kFree << 7)) : ((s1 & ~127u) | r1));
     }
@@ -623,7 +625,7 @@ wf_extend(const KernelParams kp, const WfParams wf) {
             for (uint32_t k = 0; k < 4; k++)
                 out[k].append(cls == k, fslot, lcnt + k, wf.cls_list + (size_t)k * wf.slot_stride + seg0);
         }
-        if constexpr (HC) hc.commit(hca, hcb, hq, lane);   // (collective)
+        if constexpr (HC) hc.commit(hca, hcb, count, hq, lane);   // (collective)
         // ---- prefetch the next ray of every lane that just started one -------
         if constexpr (PF) {
             const bool want = fin && mode != kDead;
