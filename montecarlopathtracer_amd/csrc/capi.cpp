@@ -20,7 +20,7 @@
 #include <vector>
 
 #include "../../include/mcpt.h"
-#include "box_quant.hpp"
+#include "half_box.hpp"
 #include "host_model.hpp"
 #include "render_launch.hpp"
 
@@ -228,7 +228,7 @@ namespace {
 
 // Device node order: treelet clusters.  A cluster holds the sibling pairs of
 // the 3 levels below its root (<= 7 pairs) contiguously, so a descent through
-// those levels stays within 112 B (16-B pairs, LDS scenes) or 224 B (32-B
+// those levels stays within 112 B (16-B pairs, LDS scenes) or 336 B (48-B
 // pair records with child boxes, global-memory scenes); clusters are emitted
 // breadth-first (the top of the tree comes first).  Slot 0 is padding and
 // slot 1 the root.  Triangles and leaf references are renumbered in the order
@@ -317,16 +317,14 @@ void build_image(mcpt_scene& s, bool force_global) {
     auto al16 = [](size_t x) { return (x + 15u) & ~size_t(15); };
     auto al128 = [](size_t x) { return (x + 127u) & ~size_t(127); };
     // Scenes that fit in LDS: 8-B node records in packed cluster order (every
-    // LDS byte counts).  Larger scenes: 32-B sibling-pair records -- the two
-    // node words plus both children's KD boxes on the root box's fixed-point
-    // grid, rounded outward (box_quant.hpp), so the traversal skips children
-    // the ray misses (child-box cull); two 16-B loads per descent step, and a
-    // record never straddles a 128-B line.
+    // LDS byte counts).  Larger scenes: 48-B sibling-pair records -- the two
+    // node words plus both children's KD boxes as fp16 rounded outward, so the
+    // traversal skips children the ray misses (child-box cull).
     DeviceOrder ord = device_order(hs);
     bool boxes = false;
     auto image_size = [&](const DeviceOrder& o, size_t& on, size_t& ol, size_t& og) {
         on = al128(size_t(nt) * 48);
-        if (boxes) ol = al16(on + size_t((o.n_slots - 1) / 2) * 32);   // pair m: device nodes 2m+1, 2m+2
+        if (boxes) ol = al16(on + size_t((o.n_slots - 1) / 2) * 48);   // pair m: device nodes 2m+1, 2m+2
         else ol = al16(on + size_t(o.n_slots + 1) * 8);                 // node slot j = device node j-1
         og = al16(ol + size_t(nl) * 4);
         // (geometries never empty for a scene with triangles; the paired
@@ -372,8 +370,6 @@ void build_image(mcpt_scene& s, bool force_global) {
                 refs[at++] = 3u * ord.tri_new[hs.leaf_ids[hs.nodes[i].leaf_begin + r]];   // record index
         }
     }
-    // the child boxes' fixed-point grid over the root box (box_quant.hpp)
-    const mcpt::BoxGrid grid = nn ? mcpt::box_grid(hs.nodes[0].bmin, hs.nodes[0].bmax) : mcpt::BoxGrid{};
     for (uint32_t i = 0; i < nn; ++i) {
         const mcpt::KdNode& n = hs.nodes[i];
         uint32_t w[2];
@@ -394,18 +390,16 @@ void build_image(mcpt_scene& s, bool force_global) {
             std::memcpy(img + off_nodes + size_t(dv + 1) * 8, w, 8);
             continue;
         }
-        // pair record: [w(left) w(right)] [box(left) box(right)]; a box = its min and max
-        // corner words on the grid, rounded outward
+        // pair record: [w(left) w(right)] [box(left) box(right)] [pad]; boxes rounded outward
         const size_t m = (dv - 1) / 2, side = (dv - 1) % 2;
-        unsigned char* rec = img + off_nodes + m * 32;
+        unsigned char* rec = img + off_nodes + m * 48;
         std::memcpy(rec + side * 8, w, 8);
-        uint32_t bw[2];
-        mcpt::box_pack(grid, n.bmin, n.bmax, bw);
-        for (int a = 0; a < 3; ++a)   // (a box outside the root box would break the cull's exactness)
-            if (!(mcpt::box_dec(grid, a, (bw[0] >> mcpt::kBoxQShift[a]) & mcpt::kBoxQMax[a]) <= n.bmin[a] &&
-                  mcpt::box_dec(grid, a, (bw[1] >> mcpt::kBoxQShift[a]) & mcpt::kBoxQMax[a]) >= n.bmax[a]))
-                throw mcpt::Error{MCPT_E_INVALID, "KD node box outside the root box"};
-        std::memcpy(rec + 16 + side * 8, bw, 8);
+        uint16_t hb[6];
+        for (int a = 0; a < 3; ++a) {
+            hb[a] = mcpt::f32_to_f16_dir(n.bmin[a], -1);
+            hb[3 + a] = mcpt::f32_to_f16_dir(n.bmax[a], +1);
+        }
+        std::memcpy(rec + 16 + side * 12, hb, 12);
     }
     for (uint32_t g = 0; g < ng; ++g) {
         const mcpt::Geometry& ge = hs.geoms[g];
@@ -427,7 +421,6 @@ void build_image(mcpt_scene& s, bool force_global) {
     gs.n_tris = nt; gs.n_nodes = nn; gs.n_leafs = nl; gs.n_geoms = ng;
     if (nn) {
         for (int a = 0; a < 3; ++a) { gs.root_min[a] = hs.nodes[0].bmin[a]; gs.root_max[a] = hs.nodes[0].bmax[a]; }
-        for (int a = 0; a < 3; ++a) { gs.box_lo[a] = grid.lo[a]; gs.box_sc[a] = grid.sc[a]; }
     }
 }
 

@@ -12,11 +12,9 @@
 //   leafs  uint32 per leaf reference: the float4 index (3 x slot) of its
 //          triangle's record -- also the index of its normals, and the ray's
 //          hit id (no multiply on the hot path)                           4 B
-//   (scenes too large for LDS: nodes are 32-B sibling-pair records instead,
-//          the two node words + both children's KD boxes, each two 32-bit
-//          corner words on GpuScene's fixed-point grid (x, y 11 bits, z 10),
-//          rounded outward (box_quant.hpp); the root's record is
-//          GpuScene::root_w)                                              32 B
+//   (scenes too large for LDS: nodes are 48-B sibling-pair records instead,
+//          the two node words + both children's KD boxes as 6 x fp16
+//          rounded outward; the root's record is GpuScene::root_w)        48 B
 //   geoms  GpuGeom per geometry (material of CUTracer.cu:300-308)      64 B
 // Shading normals live outside the image (read once per shaded hit):
 //   normals 3 x float4 per KD triangle (n0, n1, n2)                    48 B
@@ -50,11 +48,10 @@ struct GpuScene {
     const float4* normals;
     uint32_t image_bytes;
     uint32_t off_tris, off_nodes, off_leafs, off_geoms;
-    uint32_t node_boxes;                 // 1: 32-B pair records with child boxes (global-memory scenes)
+    uint32_t node_boxes;                 // 1: 48-B pair records with child boxes (global-memory scenes)
     uint32_t n_tris, n_nodes, n_leafs, n_geoms;
     float root_min[3], root_max[3];
     uint32_t root_w[2];                  // root node record (nodes[0])
-    float box_lo[3], box_sc[3];          // child-box grid: coordinate = fma(code, box_sc[a], box_lo[a])
 };
 
 // Unsigned division by a launch-invariant divisor d >= 1 as multiply-high and

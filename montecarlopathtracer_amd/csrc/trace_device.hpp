@@ -282,22 +282,16 @@ __device__ __forceinline__ float4 ld_tri(const float4* __restrict__ p) {
 #ifndef MCPT_DESCENT_CAP_GLOBAL
 #define MCPT_DESCENT_CAP_GLOBAL 5                // global-memory scenes (C4: 5 > 4)
 #endif
-// Child-box cull (scenes in global memory): each 32-B sibling-pair record also
+// Child-box cull (scenes in global memory): each sibling-pair record also
 // carries both children's KD boxes (the node region clipped to its
-// triangles' bounds, KDTree.hpp:154-155) as two corner words on a fixed-point
-// grid over the root box, rounded outward (box_quant.hpp).  A child whose box
-// the ray segment (0, best] misses is not entered: a hit that could improve
-// `best` lies inside the exact box, hence inside the stored one, and its slab
-// intervals contain t up to rounding, which the 2^-12 margins cover.
-struct BoxGridD {
-    float lx, ly, lz, sx, sy, sz;           // coordinate = fma(code, s, l) per axis (GpuScene::box_lo / box_sc)
-};
-__device__ __forceinline__ BoxGridD box_grid_of(const GpuScene& sc) {
-    return BoxGridD{sc.box_lo[0], sc.box_lo[1], sc.box_lo[2], sc.box_sc[0], sc.box_sc[1], sc.box_sc[2]};
+// triangles' bounds, KDTree.hpp:154-155) as fp16 rounded outward
+// (half_box.hpp).  A child whose box the ray segment (0, best] misses is not
+// entered: a hit that could improve `best` lies inside the exact box, hence
+// inside the stored one, and its slab intervals contain t up to rounding,
+// which the 2^-12 margins cover.
+__device__ __forceinline__ float h2f(uint32_t bits16) {
+    return (float)__builtin_bit_cast(_Float16, (unsigned short)bits16);
 }
-// a corner word's coordinates (x bits 0-10, y 11-21, z 22-31): one IEEE fma each,
-// the host's and the oracle's decode bit for bit
-__device__ __forceinline__ float qdec(uint32_t code, float s, float l) { return __builtin_fmaf((float)code, s, l); }
 // One slab of the box test for a nonzero direction component: the interval
 // update.  A zero component (the slab test degenerates to a containment test
 // of the origin) is handled by box_hit's rarely taken branch, so the six slabs
@@ -309,13 +303,13 @@ __device__ __forceinline__ void box_slab(bool zero, float o, float inv, float bl
     lo = (!zero & (a0 > lo)) ? a0 : lo;
     hi = (!zero & (a1 < hi)) ? a1 : hi;
 }
-// box = its min corner word wl and max corner word wh
-__device__ __forceinline__ bool box_hit(const RayState& r, uint32_t wl, uint32_t wh, const BoxGridD& g) {
+// box = lo.x lo.y | lo.z hi.x | hi.y hi.z as three packed fp16 pairs
+__device__ __forceinline__ bool box_hit(const RayState& r, uint32_t b0, uint32_t b1, uint32_t b2) {
     float lo = 0.0f, hi = r.best;
     const bool zx = r.d.x == 0.0f, zy = r.d.y == 0.0f, zz = r.d.z == 0.0f;
-    const float lx = qdec(wl & 0x7FFu, g.sx, g.lx), hx = qdec(wh & 0x7FFu, g.sx, g.lx);
-    const float ly = qdec((wl >> 11) & 0x7FFu, g.sy, g.ly), hy = qdec((wh >> 11) & 0x7FFu, g.sy, g.ly);
-    const float lz = qdec(wl >> 22, g.sz, g.lz), hz = qdec(wh >> 22, g.sz, g.lz);
+    const float lx = h2f(b0 & 0xFFFFu), hx = h2f(b1 >> 16);
+    const float ly = h2f(b0 >> 16), hy = h2f(b2 & 0xFFFFu);
+    const float lz = h2f(b1 & 0xFFFFu), hz = h2f(b2 >> 16);
     box_slab(zx, r.o.x, r.ix, lx, hx, lo, hi);
     box_slab(zy, r.o.y, r.iy, ly, hy, lo, hi);
     box_slab(zz, r.o.z, r.iz, lz, hz, lo, hi);
@@ -383,8 +377,7 @@ constexpr uint32_t kLeftMask = 0x3FFFFFFFu;   // inner node word: child pair ind
 template <int S, bool BOXES = false, bool COUNT = true>
 __device__ __forceinline__ int descend_steps(RayState& r, const uint2* __restrict__ nodes1, uint4* st, int stride,
                                              uint4* __restrict__ spill, uint32_t spill_stride, Counters& c,
-                                             const uint4* __restrict__ pairs, const BoxGridD& bg,
-                                             int cap MCPT_LU_PARAM) {
+                                             const uint4* __restrict__ pairs, int cap MCPT_LU_PARAM) {
     const int32_t U = stride * 16;            // one stack position (see slot_of)
     // the walk advances r.nw0/r.nw1 in place (local copies written back at
     // the cap cost register moves on every path through the loop)
@@ -397,11 +390,12 @@ __device__ __forceinline__ int descend_steps(RayState& r, const uint2* __restric
         if constexpr (COUNT) c.inner++;
         MCPT_LANE_USE(desc_w, desc_l, lu);
         const uint32_t left = w0 & kLeftMask;
-        uint4 pr, bx;
-        if constexpr (BOXES) {            // 32-B pair record: words, then box(left) and box(right) corners
-            const uint4* rec = pairs + 2u * ((left - 1u) >> 1);
+        uint4 pr, bx0, bx1;
+        if constexpr (BOXES) {            // 48-B pair record: words, box(left), box(right)
+            const uint4* rec = pairs + 3u * ((left - 1u) >> 1);
             pr = rec[0];
-            bx = rec[1];
+            bx0 = rec[1];
+            bx1 = rec[2];
         } else {
             pr = *reinterpret_cast<const uint4*>(nodes1 + left);   // children left, left+1
         }
@@ -428,8 +422,8 @@ __device__ __forceinline__ int descend_steps(RayState& r, const uint2* __restric
         bool push_it = pp | both;
         bool near_ok = true, far_ok = true;
         if constexpr (BOXES) {
-            const bool hl = box_hit(r, bx.x, bx.y, bg);
-            const bool hr = box_hit(r, bx.z, bx.w, bg);
+            const bool hl = box_hit(r, bx0.x, bx0.y, bx0.z);
+            const bool hr = box_hit(r, bx0.w, bx1.x, bx1.y);
             near_ok = below ? hl : hr;
             far_ok = below ? hr : hl;
             push_it = push_it & far_ok;
@@ -482,11 +476,10 @@ template <int S, bool BOXES = false, bool COUNT = true, bool TRIS_LDS = false, i
 __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict__ tris,
                                           const uint2* __restrict__ nodes1, const uint32_t* __restrict__ leafs,
                                           uint4* st, int stride, uint4* __restrict__ spill, uint32_t spill_stride,
-                                          Counters& c MCPT_LU_PARAM, const uint4* __restrict__ pairs = nullptr,
-                                          const BoxGridD& bg = BoxGridD{}) {
+                                          Counters& c MCPT_LU_PARAM, const uint4* __restrict__ pairs = nullptr) {
     const int32_t U = stride * 16;            // one stack position (see slot_of)
     if (r.lpos == r.lend) {                   // between leaves: descend
-        const int k = descend_steps<S, BOXES, COUNT>(r, nodes1, st, stride, spill, spill_stride, c, pairs, bg,
+        const int k = descend_steps<S, BOXES, COUNT>(r, nodes1, st, stride, spill, spill_stride, c, pairs,
                                                       CAP > 0 ? CAP : BOXES ? MCPT_DESCENT_CAP_GLOBAL : MCPT_DESCENT_CAP
                                                       MCPT_LU_ARG);
         if (k == 0) return false;
@@ -713,9 +706,7 @@ struct SlotCursor {
 
 // counters: wave reduction in 64 bits (64 lanes of 32-bit counts may exceed
 // 2^32), one atomic per wave per counter
-__device__ __forceinline__ void flush_counters(const Counters& c, unsigned long long* stats,
-                                               uint32_t lane = ~0u) {   // (lane: this lane's index, if at hand)
-    if (lane == ~0u) lane = threadIdx.x & 63u;
+__device__ __forceinline__ void flush_counters(const Counters& c, unsigned long long* stats) {
     const uint32_t vals[8] = {c.rays, c.paths, c.inner, c.leaf, c.refs, c.tests, c.shades, c.spills};
     unsigned long long sums[8];
 #pragma unroll
@@ -725,7 +716,7 @@ __device__ __forceinline__ void flush_counters(const Counters& c, unsigned long 
         for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
         sums[i] = x;
     }
-    if (lane == 0) {
+    if ((threadIdx.x & 63u) == 0) {
 #pragma unroll
         for (int i = 0; i < 8; i++)
             if (sums[i]) atomicAdd(stats + i, sums[i]);

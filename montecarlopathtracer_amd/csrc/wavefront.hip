@@ -321,7 +321,7 @@ constexpr int kWfLdsCap = MCPT_WF_DESCENT_CAP;
 #endif
 static_assert(kGlobalBlock == 256, "MCPT_WF_GLOBAL_WAVES = workgroups per CU only for one wave per SIMD each");
 #ifndef MCPT_WF_GLOBAL_PREFETCH
-#define MCPT_WF_GLOBAL_PREFETCH 0
+#define MCPT_WF_GLOBAL_PREFETCH 1
 #endif
 // register budgets (waves per SIMD the compiler plans for; 0 = none) of the
 // LDS scenes' lean extend and of the queue-order shade, and the shade's
@@ -343,91 +343,6 @@ constexpr int kLayGlobal = 0, kLayLds = 1;
 
 
 #if !MCPT_WF_PRIMARY_TU
-// Hit-id write combining (scenes in global memory, queue order;
-// MCPT_WF_HIT_COMBINE).  A lane stores its ray's 4-B hit id when the ray
-// ends, at its own time, so the L2 holds lines of the hit stream partly
-// written while the walk's node / triangle misses evict them: a C4 frame's
-// extend wrote 74.9 GB through 1.39 G fabric write requests for 14.4 GB of ids
-// (PMC, profiles/r05/calib).  Each wave reserves its queue slots 64 at a time
-// (SlotCursor), so the ids of one reservation -- a 256-B run of the hit
-// stream -- are collected in LDS (two reservations per wave in flight) and
-// stored by one coalesced wave store when the last of its rays ends.  A ray
-// that ends after its reservation's buffer was reused for a newer one (a
-// third reservation opened while it still traced) stores its id directly, and
-// the entries collected so far go out at the reuse.
-#ifndef MCPT_WF_HIT_COMBINE
-#define MCPT_WF_HIT_COMBINE 1
-#endif
-__device__ __forceinline__ uint32_t rfl(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
-struct HitCombiner {
-    static constexpr uint32_t kEmpty = 0x7FFFFFFFu;     // (ids are -1 or 3 x slot)
-    static constexpr uint32_t kFree = 0xFFFFFFu;        // chunk field of a free buffer
-    uint32_t* buf;                                      // this wave's 2 x 64 LDS words
-    // Wave-uniform state, packed (the lean extend runs at its SGPR limit, so more
-    // words would spill SGPRs into VGPR lanes): per buffer k, s_k = chunk << 7 |
-    // remaining -- the reservation's first slot / 64 (kFree: none) and the ids
-    // still to come of its slots below the queue length; bit 31 of s1: the
-    // buffer the next reservation takes.  Updated by selects and readfirstlane
-    // only: a value assigned in a branch of this structurized code is treated as
-    // divergent and held in a VGPR, which the lean extend has none of to spare.
-    uint32_t s0, s1;
-    __device__ __forceinline__ static uint32_t chunk(uint32_t sk) { return (sk >> 7) & kFree; }
-    __device__ __forceinline__ void init(uint32_t* b) {
-        buf = b;
-        s0 = s1 = kFree << 7;
-    }
-    // every lane: entry `lane` of buffer k to the hit stream if collected (a reused buffer's partial run)
-    __device__ __forceinline__ void drain(uint32_t k, uint32_t ck, int32_t* hq, uint32_t lane) {
-        __builtin_amdgcn_wave_barrier();
-        const uint32_t v = buf[k * kChunk + lane];
-        if (v != kEmpty) hq[ck * kChunk + lane] = (int32_t)v;
-    }
-    // when `isnew`: a reservation of slots [base, base + 64) of a queue of
-    // `count` rays (every lane; the queue length is a vector load, made
-    // uniform here)
-    __device__ __forceinline__ void open(bool isnew, uint32_t base_in, uint32_t count, int32_t* hq, uint32_t lane) {
-        const uint32_t base = rfl(base_in), cnt = rfl(count);
-        const bool live = isnew & (base < cnt);   // (a reservation past the queue's end: no ray is traced)
-        const uint32_t v = cnt - base < kChunk ? cnt - base : kChunk;
-        const bool k1 = (s1 >> 31) != 0u;
-        const uint32_t cold = chunk(k1 ? s1 : s0);
-        if (live & (cold != kFree)) drain(k1 ? 1u : 0u, cold, hq, lane);
-        if (live) buf[(k1 ? kChunk : 0u) + lane] = kEmpty;
-        const uint32_t sn = ((base / kChunk) << 7) | v;
-        s0 = rfl((live & !k1) ? sn : s0);
-        s1 = rfl((live & k1) ? sn : (s1 & 0x7FFFFFFFu)) | (live != k1 ? 0x80000000u : 0u);
-    }
-    // a lane whose ray ended: its hit id to its reservation's buffer (a, b: which one), or
-    // directly to the hit stream (called inside the hand-off's branch: the id needs no
-    // register beyond it)
-    __device__ __forceinline__ void put(uint32_t slot, int32_t id, int32_t* hq, bool& a, bool& b) {
-        const uint32_t c = slot / kChunk;
-        a = c == chunk(s0);
-        b = c == chunk(s1);
-        if (a | b) buf[(b ? kChunk : 0u) + (slot & (kChunk - 1u))] = (uint32_t)id;
-        else hq[slot] = id;
-    }
-    // every lane: count the ids put (a, b of the lanes whose ray ended) and store every
-    // complete reservation with one coalesced wave store
-    __device__ __forceinline__ void commit(bool a, bool b, uint32_t count, int32_t* hq, uint32_t lane) {
-        const uint32_t r0 = (s0 & 127u) - (uint32_t)__popcll(__ballot(a));
-        const uint32_t r1 = (s1 & 127u) - (uint32_t)__popcll(__ballot(b));
-        const bool f0 = (chunk(s0) != kFree) & (r0 == 0u), f1 = (chunk(s1) != kFree) & (r1 == 0u);
-        // a complete buffer holds every slot of its reservation below the queue length
-        const uint32_t cnt = rfl(count);
-        const uint32_t v0 = cnt - chunk(s0) * kChunk, v1 = cnt - chunk(s1) * kChunk;   // (>= 1 when in use)
-        if (f0 && lane < v0) hq[chunk(s0) * kChunk + lane] = (int32_t)buf[lane];
-        if (f1 && lane < v1) hq[chunk(s1) * kChunk + lane] = (int32_t)buf[kChunk + lane];
-        s0 = rfl(f0 ? (kFree << 7) : ((s0 & ~127u) | r0));
-        s1 = rfl(f1 ? ((s1 & 0x80000000u) | (kFree << 7)) : ((s1 & ~127u) | r1));
-    }
-    __device__ __forceinline__ void finish(int32_t* hq, uint32_t lane) {
-        if (chunk(s0) != kFree) drain(0u, chunk(s0), hq, lane);
-        if (chunk(s1) != kFree) drain(1u, chunk(s1), hq, lane);
-    }
-};
-constexpr size_t kHitCombineLds(int block) { return (size_t)(block / 64) * 2 * kChunk * 4; }
-
 // ---- extend: closest hit of every ray of this workgroup's segment -----------
 // COUNT = false (lean renders): the traversal counters are compiled out.
 // SORT = WfParams::sort, a template argument so that the queue-order variant
@@ -454,9 +369,7 @@ wf_extend(const KernelParams kp, const WfParams wf) {
     }
     const int tid = (int)threadIdx.x;
     const GpuScene& sc = kp.scene;
-    // LDS: [stack S x BLOCK x 16 B | scene image (kLayLds) | 5 counters (32 B) | hit-id
-    // combining buffers (HC: kLayGlobal, queue order)]
-    constexpr bool HC = MCPT_WF_HIT_COMBINE && LAY == kLayGlobal && !SORT;
+    // LDS: [stack S x BLOCK x 16 B | scene image (kLayLds) | 5 counters]
     unsigned char* const lds_image = smem + (size_t)S * BLOCK * 16;
     uint32_t* lcnt = reinterpret_cast<uint32_t*>(lds_image + (IN_LDS ? sc.image_bytes : 0u));
     if (tid < 5) lcnt[tid] = 0;
@@ -479,8 +392,7 @@ wf_extend(const KernelParams kp, const WfParams wf) {
         leafs = reinterpret_cast<const uint32_t*>(sc.image + sc.off_leafs);
         geoms = reinterpret_cast<const GpuGeom*>(sc.image + sc.off_geoms);
     }
-    const uint4* pairs = reinterpret_cast<const uint4*>(sc.image + sc.off_nodes);   // 32-B pair records (global variant)
-    const BoxGridD bg = box_grid_of(sc);
+    const uint4* pairs = reinterpret_cast<const uint4*>(sc.image + sc.off_nodes);   // 48-B pair records (global variant)
     __syncthreads();
     uint4* st = reinterpret_cast<uint4*>(smem) + tid;
     uint4* spill = kp.spill + (blockIdx.x * BLOCK + (uint32_t)tid);
@@ -498,25 +410,12 @@ wf_extend(const KernelParams kp, const WfParams wf) {
     RayState r;
     r.htri = -1;
     int mode = kDead;
-    int32_t* const hq = reinterpret_cast<int32_t*>(qb + qf(0, kQHIT, qs)) + seg0;   // this segment's hit ids
-    const uint32_t lane = (uint32_t)tid & 63u;
-    HitCombiner hc;
-    const uint32_t hc_wave = rfl((uint32_t)tid >> 6);
-    if constexpr (HC) hc.init(lcnt + 8 + hc_wave * 2u * kChunk);
-    // a slot for each lane with `want` from the wave's reservations (a new
-    // reservation opens a combining buffer)
-    auto take = [&](bool want) {
-        const uint32_t b0 = cur_chunk.base;
-        const uint32_t sl = cur_chunk.take(want, lcnt + 4);
-        if constexpr (HC) hc.open(cur_chunk.base != b0, cur_chunk.base, count, hq, lane);
-        return sl;
-    };
     // PF: the next ray of every lane is loaded a whole burst ahead (no4/nd4);
     // without it (MCPT_WF_GLOBAL_PREFETCH = 0, global-memory scenes only) a
     // finished lane loads its next ray in the hand-off, 8 VGPRs fewer
     constexpr bool PF = LAY != kLayGlobal || MCPT_WF_GLOBAL_PREFETCH;
-    uint32_t slot = take(true), depth = 0;
-    uint32_t nslot = PF ? take(true) : 0u;
+    uint32_t slot = cur_chunk.take(true, lcnt + 4), depth = 0;
+    uint32_t nslot = PF ? cur_chunk.take(true, lcnt + 4) : 0u;
     float4 no4 = make_float4(0, 0, 0, 0), nd4 = make_float4(0, 0, 0, 0);
     auto start = [&](float4 o4, float4 d4) {
         // opaque copies: the loop below must not see its ray registers as
@@ -562,7 +461,7 @@ wf_extend(const KernelParams kp, const WfParams wf) {
 #endif
             if (mode == kTrav) {
                 if (trav_iter<S, !IN_LDS, COUNT, LAY == kLayLds, IN_LDS ? kWfLdsCap : MCPT_WF_DESCENT_CAP_GLOBAL>(r, tris, nodes, leafs, st, BLOCK, spill, spill_stride, c MCPT_LU_ARG,
-                                                 pairs, bg))
+                                                 pairs))
                     mode = kReady;
             }
             const uint64_t trv = __ballot(mode == kTrav);
@@ -584,11 +483,10 @@ wf_extend(const KernelParams kp, const WfParams wf) {
             nd4 = make_float4(opaque(nd4.x), opaque(nd4.y), opaque(nd4.z), opaque(nd4.w));
         }
         const bool fin = mode == kReady;
-        const uint32_t ns0 = PF ? 0u : take(fin);   // (collective: every lane)
+        const uint32_t ns0 = PF ? 0u : cur_chunk.take(fin, lcnt + 4);   // (collective: every lane)
         uint32_t cls = 4u;
         const uint32_t fslot = slot;
         float4 hrec = make_float4(0, 0, 0, 0);
-        bool hca = false, hcb = false;   // HC: the finished ray's id went to combining buffer 0 / 1
         if (fin) {
             hrec = make_float4(r.best, r.hbeta, r.hgamma, __int_as_float(r.htri));
             cls = kClassTerminate;
@@ -611,10 +509,8 @@ wf_extend(const KernelParams kp, const WfParams wf) {
                 start(o4, d4);
             }
             if (slot >= count) mode = kDead;
-            if constexpr (!SORT && !HC)   // (r holds the next ray by now: the id from hrec)
-                hq[fslot] = __float_as_int(hrec.w);
-            else if constexpr (HC)
-                hc.put(fslot, __float_as_int(hrec.w), hq, hca, hcb);
+            if constexpr (!SORT)   // (r holds the next ray by now: the id from hrec)
+                reinterpret_cast<int32_t*>(qb + qf(0, kQHIT, qs))[seg0 + fslot] = __float_as_int(hrec.w);
             else if constexpr ((MCPT_WF_NT & 4) != 0 || (!IN_LDS && MCPT_WF_NT_HIT_GLOBAL))
                 stq_nt(&qb[qf(seg0 + fslot, kQHIT, qs)], hrec);
             else
@@ -625,11 +521,10 @@ wf_extend(const KernelParams kp, const WfParams wf) {
             for (uint32_t k = 0; k < 4; k++)
                 out[k].append(cls == k, fslot, lcnt + k, wf.cls_list + (size_t)k * wf.slot_stride + seg0);
         }
-        if constexpr (HC) hc.commit(hca, hcb, count, hq, lane);   // (collective)
         // ---- prefetch the next ray of every lane that just started one -------
         if constexpr (PF) {
             const bool want = fin && mode != kDead;
-            const uint32_t ns = take(want);
+            const uint32_t ns = cur_chunk.take(want, lcnt + 4);
             if (want) {
                 nslot = ns;
                 if (nslot < count) { no4 = ld_o(nslot); nd4 = ldq(&qb[qf(seg0 + nslot, kQD, qs)]); }
@@ -642,7 +537,6 @@ wf_extend(const KernelParams kp, const WfParams wf) {
 #pragma unroll
         for (uint32_t k = 0; k < 4; k++) out[k].flush(lcnt + k, wf.cls_list + (size_t)k * wf.slot_stride + seg0);
     }
-    if constexpr (HC) hc.finish(hq, lane);   // (every reservation is complete by now; a partial one drains)
 #ifdef MCPT_PHASE_TIMING
     if ((threadIdx.x & 63u) == 0) {
         atomicAdd(kp.stats + 8, tm_setup);
@@ -660,19 +554,9 @@ wf_extend(const KernelParams kp, const WfParams wf) {
         }
     }
 #endif
-    // (HC: the thread index from the lane and the wave, so threadIdx.x -- held in a VGPR
-    // since the kernel's start -- is dead inside the loop)
-    uint32_t lane_end = lane;
-    if constexpr (HC) asm volatile("" : "+v"(lane_end));
-    flush_counters(c, kp.stats, HC ? lane_end : ~0u);
+    flush_counters(c, kp.stats);
     __syncthreads();
-    if constexpr (HC) {
-        uint32_t l = lane;
-        asm volatile("" : "+v"(l));   // (not folded back into threadIdx.x)
-        if (hc_wave == 0u && l < 4u) cn->cls[l] = lcnt[l];
-    } else if (tid < 4) {
-        cn->cls[tid] = lcnt[tid];
-    }
+    if (tid < 4) cn->cls[tid] = lcnt[tid];
 }
 
 #endif  // !MCPT_WF_PRIMARY_TU
@@ -1190,10 +1074,6 @@ hipError_t launch_extend(const KernelParams& kp, const WfParams& wf, int grid, s
 
 // the scene image (8-B node records) is copied into LDS; an image built with
 // child-box pair records (node_boxes) is always read from global memory
-// LDS of a global-memory scene's extend workgroup: stack, 32 B of counters, the
-// hit-id combining buffers (six workgroups fit a CU's 160 KB: 6 x 26,656 B)
-constexpr size_t kWfGlobalExtendLds = (size_t)MCPT_WF_GLOBAL_S * kGlobalBlock * 16 + 32 +
-                                      (MCPT_WF_HIT_COMBINE ? kHitCombineLds(kGlobalBlock) : 0);
 bool wf_in_lds(const GpuScene& sc) { return !sc.node_boxes && lds_bytes_in_lds(sc.image_bytes, 4) + 32 <= kMaxLds; }
 
 #endif  // !MCPT_WF_PRIMARY_TU
@@ -1287,7 +1167,7 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams* wf_in, co
             // the shade's material table in LDS if it fits beside the extend's
             // workgroups on a CU (MCPT_WF_GEO_LDS)
             const size_t ext_lds = in_lds ? wf_lds_extend_bytes(kp.scene)
-                                          : (size_t)kWfGlobalSegsPerCu * kWfGlobalExtendLds;
+                                          : (size_t)kWfGlobalSegsPerCu * (MCPT_WF_GLOBAL_S * kGlobalBlock * 16 + 32);
             const size_t geo_bytes = (MCPT_WF_GEO_LDS && ext_lds + 64 * (size_t)kp.scene.n_geoms + 64 <= kLdsPerCu)
                                          ? 64 * (size_t)kp.scene.n_geoms : 0;
             // LDS scenes: one 8x8 tile of one sample per group; global-memory
@@ -1319,7 +1199,7 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams* wf_in, co
                     e = launch_extend<kLayLds, 4, kLdsBlock>(kb, wf, (int)nseg, llds, bs);
                 } else
                     e = launch_extend<kLayGlobal, MCPT_WF_GLOBAL_S, kGlobalBlock>(kb, wf, (int)nseg,
-                                                                            kWfGlobalExtendLds,
+                                                                            (size_t)MCPT_WF_GLOBAL_S * kGlobalBlock * 16 + 32,
                                                               bs);
                 if (e != hipSuccess) break;
                 if (wf.sort)

@@ -68,9 +68,8 @@ typedef struct {
                                        0: no tint (rtx.hlsl:345, the published renders) */
     int32_t mode;                   /* 0: CVMCTracer semantics; 1: QuinEngine (rtx.hlsl:304-405) */
     float proj11, proj22;           /* QE: PerspectiveFovRH scales (orc_qe_proj)  */
-    int32_t node_boxes;             /* ordered KD: skip children whose stored KD box (fixed-point
-                                       grid, rounded outward) the ray misses (the kernel does for
-                                       scenes in global memory) */
+    int32_t node_boxes;             /* ordered KD: skip children whose fp16 KD box the ray
+                                       misses (the kernel does for scenes in global memory) */
 } orc_params;
 
 typedef struct {
@@ -125,11 +124,9 @@ void orc_sample_fresnel(const float* n, const float* in, float Tr, float Ni, con
 void orc_sample_phong_qe(const float* n, const float* in, float Ns, const float* u, float* out);
 void orc_sample_fresnel_qe(const float* n, const float* in, float Tr, float Ni, const float* u, float* out);
 float orc_tan_half_fov(float fov_deg);
-/* child-box grid (csrc/box_quant.hpp): the grid over a root box, a coordinate's
- * code rounded down (dir < 0) or up (dir > 0), and a code's coordinate */
-void orc_box_grid(const float* bmin, const float* bmax, float* lo, float* sc);
-uint32_t orc_box_q(const float* lo, const float* sc, int a, float v, int dir);
-float orc_box_dec(const float* lo, const float* sc, int a, uint32_t q);
+/* binary16 of x rounded toward -inf (dir < 0) / +inf (dir > 0), and back */
+uint16_t orc_f16_dir(float x, int dir);
+float orc_f16_to_f32(uint16_t h);
 /* QE camera (GraphicsRTX.cpp:181-182): D3DXMatrixPerspectiveFovRH(fovY, W/H) diagonal */
 void orc_qe_proj(float fovy_deg, int32_t width, int32_t height, float* p11, float* p22);
 void orc_camera_basis(const float* eye, const float* dir, const float* up,
@@ -140,7 +137,7 @@ void orc_camera_basis(const float* eye, const float* dir, const float* up,
 void orc_intersect_batch(const orc_scene* s, int traversal, int64_t n,
                          const float* o, const float* d, int32_t* tri_out,
                          int32_t* geom_out, float* hit_out, orc_counters* c);
-/* same with the ordered walk's child-box cull (node_boxes) and pthreads */
+/* same with the ordered walk's fp16 child-box cull (node_boxes) and pthreads */
 void orc_intersect_batch_mt(const orc_scene* s, int traversal, int node_boxes, int threads, int64_t n,
                             const float* o, const float* d, int32_t* tri_out, int32_t* geom_out, float* hit_out,
                             orc_counters* c);

@@ -55,7 +55,6 @@ struct orc_scene {
     orc_node* nodes; int nnodes;
     uint32_t* leaf_ids; int nleaf_ids;
     int kd_depth;
-    float* qbox;            /* per node: its child-box cull box as stored (grid decode, lo3 hi3) */
 };
 
 int orc_model_read(orc_model* m, const char* path, char* err, int errlen);
@@ -63,7 +62,5 @@ int orc_model_read_tinyobj(orc_model* m, const char* path, char* err, int errlen
 void orc_model_free(orc_model* m);
 /* KD build over kd triangles (vertex triples), flattened BFS */
 void orc_kd_build(orc_scene* s);
-/* the child-box cull's stored boxes (render_ref.c, csrc/box_quant.hpp) */
-void orc_build_qboxes(orc_scene* s);
 
 #endif

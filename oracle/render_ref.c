@@ -427,58 +427,46 @@ static hit_t isect_kd_ref(qctx* q, orc_v3 o, orc_v3 d) {
 /* Ordered front-to-back traversal used by the HIP kernel:
  * split-plane intervals, conservative 2^-12 margins, full stack (<= depth). */
 
-/* =========== child boxes on the fixed-point grid (kernel mirror) ============
- * csrc/box_quant.hpp: a child box is stored as two corner words of codes on a
- * grid over the KD root box (x, y: 2047 steps, z: 1023), coordinate =
- * fmaf(code, sc[a], lo[a]); the min corner rounded down (largest code whose
- * coordinate <= the exact one), the max corner up.  Same operations as the
- * host's encoder and the kernel's decode, bit for bit.                        */
-static const uint32_t BOXQ_MAX[3] = {2047u, 2047u, 1023u};
-void orc_box_grid(const float* bmin, const float* bmax, float* lo, float* sc) {
-    for (int a = 0; a < 3; a++) {
-        const float mq = (float)BOXQ_MAX[a];
-        float v = (bmax[a] - bmin[a]) / mq;
-        if (!(v > 0.0f)) v = 0.0f;
-        while (v > 0.0f && fmaf(mq, v, bmin[a]) < bmax[a]) v = nextafterf(v, INFINITY);
-        lo[a] = bmin[a];
-        sc[a] = v;
+/* ====================== fp16 leaf boxes (kernel mirror) =================== */
+float orc_f16_to_f32(uint16_t h) {
+    uint32_t sg = (h >> 15) & 1u, e = (h >> 10) & 0x1Fu, m = h & 0x3FFu;
+    if (e == 0) {
+        float v = (float)m * 5.9604644775390625e-8f;
+        return sg ? -v : v;
     }
+    uint32_t bits = e == 31 ? ((sg << 31) | 0x7F800000u | (m << 13)) : ((sg << 31) | ((e - 15u + 127u) << 23) | (m << 13));
+    float f;
+    memcpy(&f, &bits, 4);
+    return f;
 }
-float orc_box_dec(const float* lo, const float* sc, int a, uint32_t q) { return fmaf((float)q, sc[a], lo[a]); }
-uint32_t orc_box_q(const float* lo, const float* sc, int a, float v, int dir) {
-    if (!(sc[a] > 0.0f)) return 0;
-    const int64_t mx = BOXQ_MAX[a];
-    double x = ((double)v - lo[a]) / sc[a];
-    x = dir < 0 ? floor(x) : ceil(x);
-    int64_t q = x < 0 ? 0 : (x > mx ? mx : (int64_t)x);
-    if (dir < 0) {   /* largest q with dec(q) <= v */
-        while (q > 0 && orc_box_dec(lo, sc, a, (uint32_t)q) > v) q--;
-        while (q < mx && orc_box_dec(lo, sc, a, (uint32_t)(q + 1)) <= v) q++;
-    } else {         /* smallest q with dec(q) >= v */
-        while (q < mx && orc_box_dec(lo, sc, a, (uint32_t)q) < v) q++;
-        while (q > 0 && orc_box_dec(lo, sc, a, (uint32_t)(q - 1)) >= v) q--;
+uint16_t orc_f16_dir(float x, int dir) {
+    uint32_t u;
+    memcpy(&u, &x, 4);
+    uint32_t sg = u >> 31, mag;
+    float a = x < 0 ? -x : x;
+    if (!(a < 65520.0f)) {
+        mag = 0x7C00u;
+    } else if (a < 6.103515625e-05f) {
+        mag = (uint32_t)(a * 16777216.0f);
+    } else {
+        uint32_t ua;
+        memcpy(&ua, &a, 4);
+        mag = (((ua >> 23) - 127u + 15u) << 10) | ((ua >> 13) & 0x3FFu);
+        if (mag > 0x7BFFu) mag = 0x7BFFu;
     }
-    return (uint32_t)q;
+    int up = sg ? dir < 0 : dir > 0;
+    if (mag < 0x7C00u && orc_f16_to_f32((uint16_t)mag) != a && up) mag += 1u;
+    if (mag >= 0x7C00u && !up) mag = 0x7BFFu;
+    if (mag == 0 && sg) return (uint16_t)0x8000u;
+    return (uint16_t)((sg << 15) | mag);
 }
-/* every node's stored box, decoded (built once per scene, orc_scene_load_ex) */
-void orc_build_qboxes(orc_scene* s) {
-    free(s->qbox);
-    s->qbox = malloc(sizeof(float) * 6 * (size_t)(s->nnodes ? s->nnodes : 1));
-    if (!s->nnodes) return;
-    float lo[3], sc[3];
-    orc_box_grid(s->nodes[0].bmin, s->nodes[0].bmax, lo, sc);
-    for (int n = 0; n < s->nnodes; n++)
-        for (int a = 0; a < 3; a++) {
-            s->qbox[6 * n + a] = orc_box_dec(lo, sc, a, orc_box_q(lo, sc, a, s->nodes[n].bmin[a], -1));
-            s->qbox[6 * n + 3 + a] = orc_box_dec(lo, sc, a, orc_box_q(lo, sc, a, s->nodes[n].bmax[a], +1));
-        }
-}
-/* does the ray segment (0, best] meet the node's stored box?  (trace_device.hpp box_hit) */
-static int box_hit(const float* qb, const float* oo, const float* dd, const float* inv, float best) {
+/* does the ray segment (0, best] meet the node's fp16 box?  (trace_device.hpp box_hit) */
+static int box_hit(const orc_node* nd, const float* oo, const float* dd, const float* inv, float best) {
     float lo = 0.0f, hi = best;
     int out = 0;
     for (int a = 0; a < 3; a++) {
-        float blo = qb[a], bhi = qb[3 + a];
+        float blo = orc_f16_to_f32(orc_f16_dir(nd->bmin[a], -1));
+        float bhi = orc_f16_to_f32(orc_f16_dir(nd->bmax[a], +1));
         if (dd[a] == 0.0f) {
             out |= (oo[a] < blo) | (oo[a] > bhi);
         } else {
@@ -532,8 +520,8 @@ static hit_t isect_kd_ordered(qctx* q, orc_v3 o, orc_v3 d) {
             /* child-box cull (scenes the kernel serves from global memory) */
             int nhit = 1, fhit = 1;
             if (q->node_boxes) {
-                nhit = box_hit(s->qbox + 6 * (size_t)nearc, oo, dd, inv, best);
-                fhit = box_hit(s->qbox + 6 * (size_t)farc, oo, dd, inv, best);
+                nhit = box_hit(&s->nodes[nearc], oo, dd, inv, best);
+                fhit = box_hit(&s->nodes[farc], oo, dd, inv, best);
             }
             if (dd[a] == 0.0f && oo[a] == sv) {
                 if (fhit) { st_node[sp] = farc; st_lo[sp] = tmin; st_hi[sp] = tmax; sp++; }
@@ -1005,14 +993,13 @@ orc_scene* orc_scene_load_ex(const char* path, int flavor, char* err, int errlen
         free(cv2kd);
     }
     orc_kd_build(s);
-    orc_build_qboxes(s);
     return s;
 }
 
 void orc_scene_free(orc_scene* s) {
     if (!s) return;
     orc_model_free(&s->model);
-    free(s->geoms); free(s->tri_geom); free(s->kd_tris); free(s->kd_prio); free(s->nodes); free(s->leaf_ids); free(s->qbox);
+    free(s->geoms); free(s->tri_geom); free(s->kd_tris); free(s->kd_prio); free(s->nodes); free(s->leaf_ids);
     free(s);
 }
 

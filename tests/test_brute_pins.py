@@ -1,9 +1,9 @@
-"""'Ordered KD walk (+ child-box cull) == brute force' where the product
+"""'Ordered KD walk (+ fp16 child-box cull) == brute force' where the product
 relies on it, and the scene02 statistical pin.
 
 Every GPU parity test compares the kernel with the oracle's ordered walk
 (KD_ORDERED); for scenes served from global memory (C4's 70k-triangle mesh,
-scenes 02/03) both sides also run the child-box cull.  Here that walk --
+scenes 02/03) both sides also run the fp16 child-box cull.  Here that walk --
 with the cull on and off -- is held to the brute-force restatement of
 CUTracer.cu:44-96 (every geometry, every triangle, strict t < tmin, ties in
 loop order) on >= 100k rays per scene: random rays, rays aimed at triangle

@@ -6,7 +6,7 @@ grazing rays, origins on triangle edges, rays through vertices.
 Held bit for bit (triangle id, beta, gamma, t) and counter for counter to the
 oracle's ordered walk with the same child-box cull the scene's layout uses
 (scene01 in LDS: no boxes; scenes 02/03 and the C4 mesh from global memory:
-child boxes (fixed-point grid)), and -- except where an origin sits on a triangle edge, which
+fp16 child boxes), and -- except where an origin sits on a triangle edge, which
 tests/test_brute_pins.py shows to be float artifacts of the reference's own
 arithmetic -- to the brute force of CUTracer.cu:44-96.
 """

@@ -25,7 +25,7 @@ CASES = [
 
 
 def _node_boxes(mcpt, scene_path):
-    """The kernel culls children by their stored KD boxes for scenes served from global memory."""
+    """The kernel culls children by their fp16 KD boxes for scenes served from global memory."""
     return int(mcpt.Scene(mcpt.ObjModel(scene_path), host_only=True).info()["node_boxes"])
 
 
@@ -366,7 +366,7 @@ def test_seed_sweep_matches_oracle(mcpt, oracle_mod, case, pipeline):
 
 @pytest.mark.parametrize("sc,W,H,spp", [("cornell_bunny70k", 32, 24, 2), ("scene02", 40, 30, 3), ("scene03", 40, 30, 3)])
 def test_global_memory_scenes_match_brute_force(mcpt, oracle_mod, sc, W, H, spp):
-    """The kernel's global-memory variant (ordered walk + child-box cull)
+    """The kernel's global-memory variant (ordered walk + fp16 child-box cull)
     against the oracle's brute force -- CUTracer.cu:44-96's every-triangle loop,
     no KD tree at all: identical images and ray / path / shade counts."""
     import os

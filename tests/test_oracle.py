@@ -277,8 +277,7 @@ def test_quinengine_mode_brute_equals_kd_and_is_gamma_encoded(oracle_mod, mcpt):
 
 
 def test_child_box_cull_is_exact_and_prunes(oracle_mod, mcpt):
-    """The child-box cull the kernel applies to scenes in global memory (32-B
-    pair records, boxes on the root box's fixed-point grid):
+    """The fp16 child-box cull the kernel applies to scenes in global memory:
     identical images with it on and off; most node visits and triangle tests disappear."""
     for name, sid in (("scene01", 1), ("scene02", 2), ("scene03", 2)):
         s = oracle_mod.Scene(mcpt.scene_path(name))
@@ -293,48 +292,29 @@ def test_child_box_cull_is_exact_and_prunes(oracle_mod, mcpt):
             assert cb["tri_tests"] < 0.5 * ca["tri_tests"], (name, ca["tri_tests"], cb["tri_tests"])
 
 
-def test_box_grid_rounding_contains_and_matches_product(oracle_mod, mcpt, tmp_path):
-    """The child boxes' fixed-point grid (csrc/box_quant.hpp, 32-B pair records):
-    the host encoder's grid and codes equal the oracle's (orc_box_grid /
-    orc_box_q) bit for bit, every code rounded down decodes to <= the value and
-    every code rounded up to >= it, and the two are at most one step apart --
-    on the C4 mesh's root box and a degenerate (flat) one."""
+def test_fp16_box_rounding_contains_and_matches_product(oracle_mod, tmp_path):
+    """orc_f16_dir (oracle) == mcpt::f32_to_f16_dir (csrc/half_box.hpp) bit for bit,
+    and the rounded values bracket the input."""
     import ctypes as C
     import subprocess
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(__file__), "cpp"))
     import build_dropin
+    r = np.random.default_rng(7)
+    x = np.concatenate([r.uniform(-20, 20, 20000), r.standard_normal(5000) * 1e-5,
+                        np.ldexp(r.uniform(-1, 1, 5000), r.integers(-30, 20, 5000)),
+                        [0.0, -0.0, 65504, 65519, 65520, -65520, 1e9, -1e9, 6.1035e-5, 5.9604645e-8]]).astype(np.float32)
+    src, dst = tmp_path / "x.f32", tmp_path / "h.u16"
+    x.tofile(src)
+    exe = build_dropin.build("half_box_probe")
+    out = subprocess.run([exe, str(src), str(x.size), str(dst)], capture_output=True, text=True)
+    assert out.returncode == 0, out.stderr
+    prod = np.fromfile(dst, np.uint16).reshape(-1, 2)
     L = oracle_mod.lib()
-    f3 = C.c_float * 3
-    L.orc_box_grid.argtypes = [f3, f3, f3, f3]
-    L.orc_box_q.restype = C.c_uint32
-    L.orc_box_q.argtypes = [f3, f3, C.c_int, C.c_float, C.c_int]
-    L.orc_box_dec.restype = C.c_float
-    L.orc_box_dec.argtypes = [f3, f3, C.c_int, C.c_uint32]
-    exe = build_dropin.build("box_quant_probe")
-    r = np.random.default_rng(11)
-    for bmin, bmax in (((-5.76397, 0.0, -5.0), (5.76397, 10.0, 5.0)), ((-3.9, 0.3, 1.0), (-0.7, 2.9, 1.0))):
-        lo3 = np.array(bmin, np.float32)
-        hi3 = np.array(bmax, np.float32)
-        n = 30000
-        x = (lo3 + (hi3 - lo3) * r.uniform(0, 1, (n // 3, 3)).astype(np.float32)).astype(np.float32).ravel()
-        x[:6] = np.concatenate([lo3, hi3])                     # the faces themselves
-        root, src, dst = tmp_path / "r.f32", tmp_path / "x.f32", tmp_path / "q.u32"
-        np.concatenate([lo3, hi3]).tofile(root)
-        x.tofile(src)
-        out = subprocess.run([exe, str(root), str(src), str(x.size), str(dst)], capture_output=True, text=True)
-        assert out.returncode == 0, out.stderr
-        prod = np.fromfile(dst, np.uint32)
-        glo, gsc = f3(), f3()
-        L.orc_box_grid(f3(*lo3), f3(*hi3), glo, gsc)
-        assert np.array_equal(prod[:6].view(np.float32), np.array(list(glo) + list(gsc), np.float32))
-        q = prod[6:].reshape(-1, 2)
-        for i in range(0, x.size, 7):                          # a seventh of the values through ctypes
-            a = i % 3
-            assert q[i, 0] == L.orc_box_q(glo, gsc, a, float(x[i]), -1)
-            assert q[i, 1] == L.orc_box_q(glo, gsc, a, float(x[i]), 1)
-        dec = np.array([[L.orc_box_dec(glo, gsc, i % 3, int(q[i, 0])), L.orc_box_dec(glo, gsc, i % 3, int(q[i, 1]))]
-                        for i in range(x.size)], np.float32)
-        assert np.all(dec[:, 0] <= x) and np.all(dec[:, 1] >= x)
-        assert np.all(q[:, 1] - q[:, 0] <= 1)
-        assert np.all(q[:, 1] <= np.array([2047, 2047, 1023] * (x.size // 3)))
+    L.orc_f16_dir.restype = C.c_uint16
+    L.orc_f16_dir.argtypes = [C.c_float, C.c_int]
+    ref = np.array([[L.orc_f16_dir(float(v), -1), L.orc_f16_dir(float(v), 1)] for v in x], np.uint16)
+    assert np.array_equal(prod, ref)
+    lo = ref[:, 0].view(np.float16).astype(np.float32)
+    hi = ref[:, 1].view(np.float16).astype(np.float32)
+    assert np.all(lo <= x) and np.all(hi >= x)
