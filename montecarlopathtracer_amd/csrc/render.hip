@@ -504,8 +504,7 @@ hipError_t launch_gather(const GatherParams& g, hipStream_t st) {
 
 int total_lanes_for(uint32_t image_bytes, int cus) {
     // an image that fits in LDS is built without leaf boxes (capi.cpp build_image)
-    // (MCPT_WF_DUAL: the wavefront's two rays per lane, a spill area each)
-    if (lds_bytes_in_lds(image_bytes, 4) + 32 <= kMaxLds) return cus * kLdsBlock * (MCPT_WF_DUAL ? 2 : 1);
+    if (lds_bytes_in_lds(image_bytes, 4) + 32 <= kMaxLds) return cus * kLdsBlock;
     return cus * (kGlobalBlocksPerCu > kWfGlobalSegsPerCu ? kGlobalBlocksPerCu : kWfGlobalSegsPerCu) * kGlobalBlock;
 }
 

@@ -25,12 +25,6 @@
 
 namespace mcpt {
 
-// 1: the wavefront extend of LDS scenes carries two rays per lane
-// (wavefront.hip wf_extend_dual; each with its own spill area, total_lanes_for)
-#ifndef MCPT_WF_DUAL
-#define MCPT_WF_DUAL 0
-#endif
-
 constexpr int kLdsBlock = 1024;          // in-LDS variant: one 16-wave workgroup per CU
 constexpr int kGlobalBlock = 256;        // global variant
 constexpr int kGlobalBlocksPerCu = 4;

@@ -513,121 +513,6 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
     return !pop_entry<S, !BOXES>(r, st, stride, spill, spill_stride, &top);
 }
 
-// ---- two rays per lane (MCPT_WF_DUAL experiment, scenes in LDS) -----------
-// One inner-node step of the ordered walk on 8-B node words (descend_steps'
-// body): the node in (r.nw0, r.nw1), its children's pair record pr; the far
-// child is pushed when both are needed, the node words advance to the child
-// entered.
-template <int S, bool COUNT>
-__device__ __forceinline__ void kd_step(RayState& r, const uint4 pr, uint4* st, int stride, uint4* __restrict__ spill,
-                                        uint32_t spill_stride, Counters& c) {
-    const int32_t U = stride * 16;
-    const int a = (int)(r.nw0 >> 30);
-    const float sv = __uint_as_float(r.nw1);
-    const float oa = sel3(a, r.o.x, r.o.y, r.o.z);
-    const float ia = sel3(a, r.ix, r.iy, r.iz);
-    const float t = (sv - oa) * ia;
-    bool below = oa < sv, pp = false;
-    if (__builtin_expect(oa == sv, 0)) {
-        const float da = sel3(a, r.d.x, r.d.y, r.d.z);
-        below = da <= 0.0f;
-        pp = da == 0.0f;
-    }
-    const float te = t * kEpsHi;
-    const bool no = !(t > 0.0f) | (t > r.tmax);
-    const bool fo = te < r.tmin;
-    const bool go_far = !pp & !no & fo;
-    const bool both = !pp & !no & !fo;
-    const bool push_it = pp | both;
-    const uint32_t f0 = below ? pr.z : pr.x, f1 = below ? pr.w : pr.y;
-    if (push_it) {
-        const float plo = max_qnan(t, r.tmin);
-        lds_uint4* slot = slot_of<S>(st, stride, r.sp);
-        if (r.sp - r.lo == S * U) {
-            spill[((uint32_t)r.lo / (uint32_t)U) * spill_stride] = ld4(slot);
-            r.lo += U;
-            if constexpr (COUNT) c.spills++;
-        }
-        st4(slot, make_uint4(f0, f1, __float_as_uint(plo), __float_as_uint(r.tmax)));
-        r.sp += U;
-        r.tmax = min_qnan(te, r.tmax);
-    }
-    const bool enter_left = below != go_far;
-    r.nw0 = enter_left ? pr.x : pr.z;
-    r.nw1 = enter_left ? pr.y : pr.w;
-}
-// One resumable traversal call for the two rays a, b of a lane (ta, tb: the ray
-// is traversing), per ray exactly trav_iter's state changes: the descents of
-// both rays advance in one loop -- each iteration reads both rays' pair records
-// before either step runs, so one LDS round trip serves two steps -- then each
-// ray's leaf pair and pop.  Returns bit 0 / bit 1: ray a / b has its final hit.
-template <int S, bool COUNT, int CAP>
-__device__ __forceinline__ uint32_t trav_iter_dual(RayState& a, RayState& b, bool ta, bool tb,
-                                                   const float4* __restrict__ tris, const uint2* __restrict__ nodes1,
-                                                   const uint32_t* __restrict__ leafs, uint4* sta, uint4* stb,
-                                                   int stride, uint4* __restrict__ spa, uint4* __restrict__ spb,
-                                                   uint32_t spill_stride, Counters& c) {
-    const int32_t U = stride * 16;
-    const bool da = ta & (a.lpos == a.lend), db = tb & (b.lpos == b.lend);
-#pragma unroll 1
-    for (int i = 0; i < CAP; i++) {
-        const bool sa = da & ((a.nw0 >> 30) != 3u), sb = db & ((b.nw0 >> 30) != 3u);
-        if (!__ballot(sa | sb)) break;
-        uint4 pa = make_uint4(0, 0, 0, 0), pb = pa;
-        if (sa) pa = *reinterpret_cast<const uint4*>(nodes1 + (a.nw0 & kLeftMask));
-        if (sb) pb = *reinterpret_cast<const uint4*>(nodes1 + (b.nw0 & kLeftMask));
-        if (sa) {
-            if constexpr (COUNT) c.inner++;
-            kd_step<S, COUNT>(a, pa, sta, stride, spa, spill_stride, c);
-        }
-        if (sb) {
-            if constexpr (COUNT) c.inner++;
-            kd_step<S, COUNT>(b, pb, stb, stride, spb, spill_stride, c);
-        }
-    }
-    // a descending ray now at a leaf takes its refs; one still inside is capped
-    bool ga = ta, gb = tb;                    // the ray goes on to its leaf's tests / pop
-    if (da) {
-        if ((a.nw0 >> 30) == 3u) {
-            if constexpr (COUNT) c.leaf++;
-            a.lpos = a.nw0 & 0x3FFFFFFFu;
-            a.lend = a.lpos + a.nw1;
-        } else {
-            ga = false;
-        }
-    }
-    if (db) {
-        if ((b.nw0 >> 30) == 3u) {
-            if constexpr (COUNT) c.leaf++;
-            b.lpos = b.nw0 & 0x3FFFFFFFu;
-            b.lend = b.lpos + b.nw1;
-        } else {
-            gb = false;
-        }
-    }
-    uint32_t res = 0;
-    auto leaf_and_pop = [&](RayState& r, uint4* st, uint4* sp) -> bool {
-        const uint4 top = ld4(slot_of<S>(st, stride, r.sp - U));
-        if (r.lpos < r.lend) {
-            const bool two = r.lend - r.lpos >= 2u;
-            const uint32_t k0 = leafs[r.lpos], k1n = leafs[r.lpos + 1u];
-            const uint32_t k1 = two ? k1n : k0;
-            const float4 a0 = ld_tri<true>(tris + k0), a1 = ld_tri<true>(tris + k0 + 1);
-            const float4 a2 = ld_tri<true>(tris + k0 + 2), b0 = ld_tri<true>(tris + k1);
-            const float4 b1 = ld_tri<true>(tris + k1 + 1), b2 = ld_tri<true>(tris + k1 + 2);
-            if constexpr (COUNT) c.refs += two ? 2u : 1u;
-            if constexpr (COUNT) c.tests += two ? 2u : 1u;
-            test_tri_pair<false>(r, a0, a1, a2, k0, b0, b1, b2, k1, two);
-            r.lpos += two ? 2u : 1u;
-        }
-        if (r.lpos < r.lend) return false;
-        return !pop_entry<S, true>(r, st, stride, sp, spill_stride, &top);
-    };
-    if (ga && leaf_and_pop(a, sta, spa)) res |= 1u;
-    if (gb && leaf_and_pop(b, stb, spb)) res |= 2u;
-    return res;
-}
-
 // work unit v (packed owned-pixel index) -> image pixel; false outside the image
 __device__ __forceinline__ bool unit_pixel(const KernelParams& kp, uint32_t v, int& x, int& y) {
     const uint32_t k = kp.div_tt.div(v), w = v - k * kp.div_tt.d;

@@ -559,130 +559,6 @@ wf_extend(const KernelParams kp, const WfParams wf) {
     if (tid < 4) cn->cls[tid] = lcnt[tid];
 }
 
-// ---- extend with two rays per lane (MCPT_WF_DUAL, LDS scenes, queue order) ---
-// latency tolerance at the fixed occupancy the LDS image
-// allows (one 1024-thread workgroup per CU, four waves per SIMD): every lane
-// carries two rays, a and b, each with its own 2-entry LDS stack (the 64 KB of
-// 4-entry stacks, split) and spill area, and one traversal call advances both
-// (trav_iter_dual: their descents in one loop, both pair records requested
-// before either step).  Hand-off, prefetch and hit stores per ray as in
-// wf_extend; same walk per ray, so the same hits and counters.
-template <int BLOCK, bool COUNT>
-__global__ void __launch_bounds__(BLOCK, 1) wf_extend_dual(const KernelParams kp, const WfParams wf) {
-    constexpr int S2 = 2;                                 // LDS stack entries per ray
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const uint32_t g = blockIdx.x;
-    WfCounters* cn = wf.cnt + (size_t)wf.bounce * wf.nseg + g;
-    const uint32_t count = g < wf.nseg ? cn->queued : 0u;
-    if (count == 0) {
-        if (g < wf.nseg && threadIdx.x < 4) cn->cls[threadIdx.x] = 0;
-        return;
-    }
-    const int tid = (int)threadIdx.x;
-    const GpuScene& sc = kp.scene;
-    unsigned char* const lds_image = smem + (size_t)2 * S2 * BLOCK * 16;
-    uint32_t* lcnt = reinterpret_cast<uint32_t*>(lds_image + sc.image_bytes);
-    if (tid < 5) lcnt[tid] = 0;
-    {
-        const uint4* src = reinterpret_cast<const uint4*>(sc.image);
-        uint4* dst = reinterpret_cast<uint4*>(lds_image);
-        const uint32_t n16 = sc.image_bytes / 16u;
-        for (uint32_t i = (uint32_t)tid; i < n16; i += BLOCK) dst[i] = src[i];
-    }
-    const float4* tris = reinterpret_cast<const float4*>(lds_image + sc.off_tris);
-    const uint2* nodes = reinterpret_cast<const uint2*>(lds_image + sc.off_nodes) + 1;
-    const uint32_t* leafs = reinterpret_cast<const uint32_t*>(lds_image + sc.off_leafs);
-    __syncthreads();
-    uint4* sta = reinterpret_cast<uint4*>(smem) + tid;               // rows 0-1
-    uint4* stb = sta + S2 * BLOCK;                                    // rows 2-3
-    const uint32_t spill_stride = kp.total_lanes;                     // (2 x the lanes: a, then b)
-    uint4* spa = kp.spill + (blockIdx.x * BLOCK + (uint32_t)tid);
-    uint4* spb = spa + spill_stride / 2u;
-    const size_t seg0 = (size_t)g * wf.seg;
-    float4* qb = wf.q[wf.bounce & 1];
-    const uint32_t qs = wf.slot_stride;
-    int32_t* const hq = reinterpret_cast<int32_t*>(qb + qf(0, kQHIT, qs)) + seg0;
-    Counters c = {0, 0, 0, 0, 0, 0, 0, 0};
-    SlotCursor cur_chunk = {0, kChunk};
-    RayState ra, rb;
-    ra.htri = rb.htri = -1;
-    int ma = kDead, mb = kDead;
-    int refill;
-    asm volatile("s_mov_b32 %0, %1" : "=s"(refill) : "s"(wf.refill_thresh));
-    const bool eye0 = MCPT_WF_IMPLICIT0 >= 2 && wf.bounce == 0 && implicit0(kp, wf);
-    const float4 eye4 = make_float4(kp.eye[0], kp.eye[1], kp.eye[2], 0.0f);
-    auto ld_o = [&](uint32_t sl) { return eye0 ? eye4 : ldq(&qb[qf(seg0 + sl, kQO, qs)]); };
-    auto start = [&](RayState& r, int& m, float4 o4, float4 d4) {
-        r.o = v3(opaque(o4.x), opaque(o4.y), opaque(o4.z));
-        r.d = v3(opaque(d4.x), opaque(d4.y), opaque(d4.z));
-        const bool live = begin_ray(r, sc, kp.best_init);
-        m = (__float_as_uint(d4.w) != kNoRay && live) ? kTrav : kReady;
-    };
-    // slots: a's, b's, then each ray's prefetched next one
-    uint32_t sla = cur_chunk.take(true, lcnt + 4), slb = cur_chunk.take(true, lcnt + 4);
-    uint32_t nsa = cur_chunk.take(true, lcnt + 4), nsb = cur_chunk.take(true, lcnt + 4);
-    float4 noa = make_float4(0, 0, 0, 0), nda = noa, nob = noa, ndb = noa;
-    if (sla < count) start(ra, ma, ld_o(sla), ldq(&qb[qf(seg0 + sla, kQD, qs)]));
-    if (slb < count) start(rb, mb, ld_o(slb), ldq(&qb[qf(seg0 + slb, kQD, qs)]));
-    if (nsa < count) { noa = ld_o(nsa); nda = ldq(&qb[qf(seg0 + nsa, kQD, qs)]); }
-    if (nsb < count) { nob = ld_o(nsb); ndb = ldq(&qb[qf(seg0 + nsb, kQD, qs)]); }
-    for (;;) {
-        __builtin_amdgcn_s_setprio(MCPT_WF_EXT_PRIO);
-        for (;;) {
-            const bool ta = ma == kTrav, tb = mb == kTrav;
-            if (ta | tb) {
-                const uint32_t f = trav_iter_dual<S2, COUNT, kWfLdsCap>(ra, rb, ta, tb, tris, nodes, leafs, sta, stb,
-                                                                        BLOCK, spa, spb, spill_stride, c);
-                if (f & 1u) ma = kReady;
-                if (f & 2u) mb = kReady;
-            }
-            const uint64_t trv = __ballot(ma == kTrav) | __ballot(mb == kTrav);
-            const int rdy = (int)__popcll(__ballot(ma == kReady)) + (int)__popcll(__ballot(mb == kReady));
-            if (!trv || rdy >= refill) break;
-        }
-        __builtin_amdgcn_s_setprio(MCPT_WF_EXT_PRIO + 1);
-        noa = make_float4(opaque(noa.x), opaque(noa.y), opaque(noa.z), opaque(noa.w));
-        nda = make_float4(opaque(nda.x), opaque(nda.y), opaque(nda.z), opaque(nda.w));
-        nob = make_float4(opaque(nob.x), opaque(nob.y), opaque(nob.z), opaque(nob.w));
-        ndb = make_float4(opaque(ndb.x), opaque(ndb.y), opaque(ndb.z), opaque(ndb.w));
-        const bool fa = ma == kReady, fb = mb == kReady;
-        if (fa) {
-            const int32_t id = ra.htri;
-            const uint32_t fs = sla;
-            sla = nsa;
-            start(ra, ma, noa, nda);
-            if (sla >= count) ma = kDead;
-            hq[fs] = id;
-        }
-        if (fb) {
-            const int32_t id = rb.htri;
-            const uint32_t fs = slb;
-            slb = nsb;
-            start(rb, mb, nob, ndb);
-            if (slb >= count) mb = kDead;
-            hq[fs] = id;
-        }
-        {
-            const bool wa = fa && ma != kDead;
-            const uint32_t n = cur_chunk.take(wa, lcnt + 4);
-            if (wa) {
-                nsa = n;
-                if (nsa < count) { noa = ld_o(nsa); nda = ldq(&qb[qf(seg0 + nsa, kQD, qs)]); }
-            }
-            const bool wb = fb && mb != kDead;
-            const uint32_t n2 = cur_chunk.take(wb, lcnt + 4);
-            if (wb) {
-                nsb = n2;
-                if (nsb < count) { nob = ld_o(nsb); ndb = ldq(&qb[qf(seg0 + nsb, kQD, qs)]); }
-            }
-        }
-        if (!__ballot((ma != kDead) | (mb != kDead))) break;
-    }
-    flush_counters(c, kp.stats);
-    __syncthreads();
-    if (tid < 4) cn->cls[tid] = lcnt[tid];
-}
-
 #endif  // !MCPT_WF_PRIMARY_TU
 
 // ---- extend of bounce 0, wave-coherent (CV mode, queue-order shade) ---------
@@ -1196,16 +1072,6 @@ hipError_t launch_extend(const KernelParams& kp, const WfParams& wf, int grid, s
     return hipGetLastError();
 }
 
-template <int BLOCK>
-hipError_t launch_extend_dual(const KernelParams& kp, const WfParams& wf, int grid, size_t lds, hipStream_t st) {
-    auto kern = kp.lean ? wf_extend_dual<BLOCK, false> : wf_extend_dual<BLOCK, true>;
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(BLOCK), lds, st, kp, wf);
-    return hipGetLastError();
-}
-
 // the scene image (8-B node records) is copied into LDS; an image built with
 // child-box pair records (node_boxes) is always read from global memory
 bool wf_in_lds(const GpuScene& sc) { return !sc.node_boxes && lds_bytes_in_lds(sc.image_bytes, 4) + 32 <= kMaxLds; }
@@ -1329,8 +1195,6 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams* wf_in, co
                 const size_t llds = in_lds ? wf_lds_extend_bytes(kb.scene) : 0;
                 if (packet && b == 0) {
                     e = launch_wavefront_primary(kb, wf, (int)nseg, llds, bs);
-                } else if (in_lds && MCPT_WF_DUAL && !wf.sort) {
-                    e = launch_extend_dual<kLdsBlock>(kb, wf, (int)nseg, llds, bs);
                 } else if (in_lds) {
                     e = launch_extend<kLayLds, 4, kLdsBlock>(kb, wf, (int)nseg, llds, bs);
                 } else
