@@ -20,7 +20,7 @@ SOURCES = ["host_model.cpp", "kd_cache.cpp", "capi.cpp", "render.hip", "wavefron
 # per-source code generation (wavefront_primary.hip: the bounce-0 packet extend's
 # wave-uniform control flow as scalar branches)
 SOURCE_FLAGS = {"wavefront_primary.hip": ["-mllvm", "-structurizecfg-skip-uniform-regions=1"]}
-HEADERS = ["host_model.hpp", "mcpt_device.hpp", "render_launch.hpp", "trace_device.hpp", "half_box.hpp", "leaf_box.hpp"]
+HEADERS = ["host_model.hpp", "mcpt_device.hpp", "render_launch.hpp", "trace_device.hpp", "half_box.hpp"]
 ARCH = os.environ.get("MCPT_OFFLOAD_ARCH", "gfx950")
 
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-fno-slp-vectorize", "-Wall",

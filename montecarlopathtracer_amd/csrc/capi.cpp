@@ -21,7 +21,6 @@
 
 #include "../../include/mcpt.h"
 #include "half_box.hpp"
-#include "leaf_box.hpp"
 #include "host_model.hpp"
 #include "render_launch.hpp"
 
@@ -371,9 +370,6 @@ void build_image(mcpt_scene& s, bool force_global) {
                 refs[at++] = 3u * ord.tri_new[hs.leaf_ids[hs.nodes[i].leaf_begin + r]];   // record index
         }
     }
-    // 8-B node images: leaf words carry the leaf's box (leaf_box.hpp), so the
-    // walk culls a leaf the ray misses before reading its refs
-    const mcpt::LeafBoxPack lbp = boxes ? mcpt::LeafBoxPack{} : mcpt::leaf_box_pack(hs);
     for (uint32_t i = 0; i < nn; ++i) {
         const mcpt::KdNode& n = hs.nodes[i];
         uint32_t w[2];
@@ -381,12 +377,8 @@ void build_image(mcpt_scene& s, bool force_global) {
             w[0] = ((n.axis - 1u) << 30) | ord.node_new[n.left];
             std::memcpy(&w[1], &n.split, 4);
         } else {
-            if (lbp.qb) {
-                mcpt::leaf_word(lbp, leaf_begin_new[i], n.leaf_count, n.bmin, n.bmax, w);
-            } else {
-                w[0] = (3u << 30) | leaf_begin_new[i];
-                w[1] = n.leaf_count;
-            }
+            w[0] = (3u << 30) | leaf_begin_new[i];
+            w[1] = n.leaf_count;
         }
         const uint32_t dv = ord.node_new[i];
         if (i == 0) {
@@ -429,8 +421,6 @@ void build_image(mcpt_scene& s, bool force_global) {
     gs.n_tris = nt; gs.n_nodes = nn; gs.n_leafs = nl; gs.n_geoms = ng;
     if (nn) {
         for (int a = 0; a < 3; ++a) { gs.root_min[a] = hs.nodes[0].bmin[a]; gs.root_max[a] = hs.nodes[0].bmax[a]; }
-        gs.leaf_qb = lbp.qb; gs.leaf_rb = lbp.rb; gs.leaf_cb = lbp.cb;
-        for (int a = 0; a < 3; ++a) { gs.leaf_lo[a] = lbp.lo[a]; gs.leaf_sc[a] = lbp.sc[a]; }
     }
 }
 

@@ -87,7 +87,6 @@ __global__ void __launch_bounds__(BLOCK, (!IN_LDS && COUNT) ? 4 : 1) path_kernel
         geoms = reinterpret_cast<const GpuGeom*>(sc.image + sc.off_geoms);
     }
     const uint4* pairs = reinterpret_cast<const uint4*>(sc.image + sc.off_nodes);   // 48-B pair records (global variant)
-    const LeafBoxD lb = leaf_box_of(sc);
     uint4* st = reinterpret_cast<uint4*>(smem) + tid;   // [S][BLOCK] x 16 B
     const uint32_t gl = blockIdx.x * BLOCK + (uint32_t)tid;
     uint4* spill = kp.spill + gl;
@@ -292,8 +291,7 @@ __global__ void __launch_bounds__(BLOCK, (!IN_LDS && COUNT) ? 4 : 1) path_kernel
             }
 #endif
             if (mode == kTrav) {
-                if (trav_iter<S, !IN_LDS, COUNT, IN_LDS>(r, tris, nodes, leafs, st, BLOCK, spill, spill_stride, c MCPT_LU_ARG, pairs,
-                                                         lb))
+                if (trav_iter<S, !IN_LDS, COUNT, IN_LDS>(r, tris, nodes, leafs, st, BLOCK, spill, spill_stride, c MCPT_LU_ARG, pairs))
                     mode = kReady;
             }
             const uint64_t trv = __ballot(mode == kTrav);
@@ -403,7 +401,6 @@ __global__ void __launch_bounds__(kQueryBlock) query_kernel(const QueryParams q)
     const uint2* nodes = reinterpret_cast<const uint2*>(sc.image + sc.off_nodes) + 1;
     const uint32_t* leafs = reinterpret_cast<const uint32_t*>(sc.image + sc.off_leafs);
     const uint4* pairs = reinterpret_cast<const uint4*>(sc.image + sc.off_nodes);
-    const LeafBoxD lb = leaf_box_of(sc);
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0};
 #ifdef MCPT_PHASE_TIMING
     LaneUse lu = {0, 0, 0, 0, 0, 0};
@@ -414,7 +411,7 @@ __global__ void __launch_bounds__(kQueryBlock) query_kernel(const QueryParams q)
     if (live) c.rays++;
     if (begin_ray(r, sc, q.best_init) && live)
         while (!trav_iter<S, BOXES, true>(r, tris, nodes, leafs, stk + tid, kQueryBlock, q.spill + i, q.n,
-                                          c MCPT_LU_ARG, pairs, lb)) {
+                                          c MCPT_LU_ARG, pairs)) {
         }
     if (live) {
         q.slot[i] = r.htri < 0 ? -1 : r.htri / 3;

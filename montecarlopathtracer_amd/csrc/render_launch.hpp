@@ -8,8 +8,7 @@
 //   nodes  uint2 per KD node (BFS), stored one slot late so that every
 //          sibling pair (left, left+1; left is odd in BFS order) is one aligned
 //          16-B record: inner x = axis<<30 | left child, y = split value bits;
-//          leaf x = 3<<30 | first leaf ref | count | 2 box codes, y = 4 box
-//          codes (the leaf's KD box on a coarse grid, leaf_box.hpp)       8 B
+//          leaf x = 3<<30 | first leaf ref, y = count                       8 B
 //   leafs  uint32 per leaf reference: the float4 index (3 x slot) of its
 //          triangle's record -- also the index of its normals, and the ray's
 //          hit id (no multiply on the hot path)                           4 B
@@ -53,10 +52,6 @@ struct GpuScene {
     uint32_t n_tris, n_nodes, n_leafs, n_geoms;
     float root_min[3], root_max[3];
     uint32_t root_w[2];                  // root node record (nodes[0])
-    // 8-B node images: leaf words pack [first ref : rb | count : cb | box] (leaf_box.hpp);
-    // leaf_qb = box bits per coordinate (0: plain leaf words, no leaf-box cull)
-    uint32_t leaf_qb, leaf_rb, leaf_cb;
-    float leaf_lo[3], leaf_sc[3];        // leaf-box grid: coordinate = fma(code, leaf_sc[a], leaf_lo[a])
 };
 
 // Unsigned division by a launch-invariant divisor d >= 1 as multiply-high and

@@ -369,51 +369,6 @@ __device__ __forceinline__ bool pop_entry(RayState& r, uint4* st, int stride, ui
 
 constexpr uint32_t kLeftMask = 0x3FFFFFFFu;   // inner node word: child pair index
 
-// Leaf boxes in the leaf words of 8-B node images (leaf_box.hpp): a ray that
-// reaches a leaf tests (0, best] against the leaf's box -- six qb-bit codes on
-// a grid over the root box, decoded by one IEEE fma each as the host and the
-// oracle do -- and skips the leaf's refs and triangles when it misses.
-struct LeafBoxD {
-    uint32_t qb, rb, cb;                  // box bits per coordinate (0: plain leaf words), ref bits, count bits
-    float lx, ly, lz, sx, sy, sz;         // coordinate = fma(code, s, l)
-};
-__device__ __forceinline__ LeafBoxD leaf_box_of(const GpuScene& sc) {
-    return LeafBoxD{sc.leaf_qb, sc.leaf_rb, sc.leaf_cb, sc.leaf_lo[0], sc.leaf_lo[1], sc.leaf_lo[2],
-                    sc.leaf_sc[0],  sc.leaf_sc[1], sc.leaf_sc[2]};
-}
-__device__ __forceinline__ uint32_t ubfe(uint32_t x, uint32_t off, uint32_t w) {
-    return __builtin_amdgcn_ubfe(x, off, w);
-}
-// the refs [lpos, lend) of the leaf with words (w0, w1), and whether the ray
-// (origin o, inverse direction inv, best hit so far) meets its box; zero
-// direction components test the origin against their slab
-__device__ __forceinline__ bool leaf_open(const LeafBoxD& lb, uint32_t w0, uint32_t w1, V3 o, V3 d, float ix,
-                                          float iy, float iz, float best, uint32_t& lpos, uint32_t& lend) {
-    if (lb.qb == 0u) {                       // (uniform) plain leaf words
-        lpos = w0 & 0x3FFFFFFFu;
-        lend = lpos + w1;
-        return true;
-    }
-    lpos = ubfe(w0, 0u, lb.rb);
-    lend = lpos + ubfe(w0, lb.rb, lb.cb);
-    const uint32_t q = lb.qb;
-    const float xl = __builtin_fmaf((float)ubfe(w1, 0u, q), lb.sx, lb.lx);
-    const float yl = __builtin_fmaf((float)ubfe(w1, q, q), lb.sy, lb.ly);
-    const float zl = __builtin_fmaf((float)ubfe(w1, 2u * q, q), lb.sz, lb.lz);
-    const float xh = __builtin_fmaf((float)ubfe(w1, 3u * q, q), lb.sx, lb.lx);
-    const float yh = __builtin_fmaf((float)ubfe(w0, 30u - 2u * q, q), lb.sy, lb.ly);
-    const float zh = __builtin_fmaf((float)ubfe(w0, 30u - q, q), lb.sz, lb.lz);
-    float lo = 0.0f, hi = best;
-    const bool zx = d.x == 0.0f, zy = d.y == 0.0f, zz = d.z == 0.0f;
-    box_slab(zx, o.x, ix, xl, xh, lo, hi);
-    box_slab(zy, o.y, iy, yl, yh, lo, hi);
-    box_slab(zz, o.z, iz, zl, zh, lo, hi);
-    bool out = false;
-    if (__builtin_expect(zx | zy | zz, 0))
-        out = (zx & ((o.x < xl) | (o.x > xh))) | (zy & ((o.y < yl) | (o.y > yh))) | (zz & ((o.z < zl) | (o.z > zh)));
-    return !out && !(lo * kEpsLo > hi * kEpsHi);
-}
-
 // Descent of a ray between leaves: at most `cap` inner-node steps (the node
 // record and interval stay in the ray state); 0 = cap reached mid-descent,
 // 1 = a leaf reached (its refs in [lpos, lend)), 2 = the walk ended (a
@@ -422,8 +377,7 @@ __device__ __forceinline__ bool leaf_open(const LeafBoxD& lb, uint32_t w0, uint3
 template <int S, bool BOXES = false, bool COUNT = true>
 __device__ __forceinline__ int descend_steps(RayState& r, const uint2* __restrict__ nodes1, uint4* st, int stride,
                                              uint4* __restrict__ spill, uint32_t spill_stride, Counters& c,
-                                             const uint4* __restrict__ pairs, const LeafBoxD& lb,
-                                             int cap MCPT_LU_PARAM) {
+                                             const uint4* __restrict__ pairs, int cap MCPT_LU_PARAM) {
     const int32_t U = stride * 16;            // one stack position (see slot_of)
     // the walk advances r.nw0/r.nw1 in place (local copies written back at
     // the cap cost register moves on every path through the loop)
@@ -509,15 +463,8 @@ __device__ __forceinline__ int descend_steps(RayState& r, const uint2* __restric
         }
     }
     if constexpr (COUNT) c.leaf++;
-    if constexpr (BOXES) {
-        r.lpos = w0 & 0x3FFFFFFFu;
-        r.lend = r.lpos + w1;
-    } else {                                  // leaf-box cull: a missed leaf has nothing to test
-        uint32_t lpos, lend;
-        const bool hit = leaf_open(lb, w0, w1, r.o, r.d, r.ix, r.iy, r.iz, r.best, lpos, lend);
-        r.lpos = lpos;
-        r.lend = hit ? lend : lpos;
-    }
+    r.lpos = w0 & 0x3FFFFFFFu;
+    r.lend = r.lpos + w1;
     return 1;
 }
 
@@ -529,11 +476,10 @@ template <int S, bool BOXES = false, bool COUNT = true, bool TRIS_LDS = false, i
 __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict__ tris,
                                           const uint2* __restrict__ nodes1, const uint32_t* __restrict__ leafs,
                                           uint4* st, int stride, uint4* __restrict__ spill, uint32_t spill_stride,
-                                          Counters& c MCPT_LU_PARAM, const uint4* __restrict__ pairs = nullptr,
-                                          const LeafBoxD& lb = LeafBoxD{}) {
+                                          Counters& c MCPT_LU_PARAM, const uint4* __restrict__ pairs = nullptr) {
     const int32_t U = stride * 16;            // one stack position (see slot_of)
     if (r.lpos == r.lend) {                   // between leaves: descend
-        const int k = descend_steps<S, BOXES, COUNT>(r, nodes1, st, stride, spill, spill_stride, c, pairs, lb,
+        const int k = descend_steps<S, BOXES, COUNT>(r, nodes1, st, stride, spill, spill_stride, c, pairs,
                                                       CAP > 0 ? CAP : BOXES ? MCPT_DESCENT_CAP_GLOBAL : MCPT_DESCENT_CAP
                                                       MCPT_LU_ARG);
         if (k == 0) return false;

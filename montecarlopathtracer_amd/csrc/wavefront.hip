@@ -393,7 +393,6 @@ wf_extend(const KernelParams kp, const WfParams wf) {
         geoms = reinterpret_cast<const GpuGeom*>(sc.image + sc.off_geoms);
     }
     const uint4* pairs = reinterpret_cast<const uint4*>(sc.image + sc.off_nodes);   // 48-B pair records (global variant)
-    const LeafBoxD lb = leaf_box_of(sc);
     __syncthreads();
     uint4* st = reinterpret_cast<uint4*>(smem) + tid;
     uint4* spill = kp.spill + (blockIdx.x * BLOCK + (uint32_t)tid);
@@ -462,7 +461,7 @@ wf_extend(const KernelParams kp, const WfParams wf) {
 #endif
             if (mode == kTrav) {
                 if (trav_iter<S, !IN_LDS, COUNT, LAY == kLayLds, IN_LDS ? kWfLdsCap : MCPT_WF_DESCENT_CAP_GLOBAL>(r, tris, nodes, leafs, st, BLOCK, spill, spill_stride, c MCPT_LU_ARG,
-                                                 pairs, lb))
+                                                 pairs))
                     mode = kReady;
             }
             const uint64_t trv = __ballot(mode == kTrav);
@@ -627,7 +626,6 @@ __global__ void __launch_bounds__(BLOCK, 1) wf_extend_primary(const KernelParams
     const float4* tris = reinterpret_cast<const float4*>(lds_image + sc.off_tris);
     const uint2* nodes = reinterpret_cast<const uint2*>(lds_image + sc.off_nodes) + 1;
     const uint32_t* leafs = reinterpret_cast<const uint32_t*>(lds_image + sc.off_leafs);
-    const LeafBoxD lb = leaf_box_of(sc);
     __syncthreads();
     uint4* st = reinterpret_cast<uint4*>(smem) + tid;
     uint4* spill = kp.spill + (blockIdx.x * BLOCK + (uint32_t)tid);
@@ -773,15 +771,9 @@ __global__ void __launch_bounds__(BLOCK, 1) wf_extend_primary(const KernelParams
                     continue;
                 }
                 // ---- leaf: the active lanes test its triangles, two per round ----
-                // (a lane whose ray misses the leaf's box tests none, as its own
-                // walk's leaf-box cull: leaf_open)
                 {
-                    uint32_t lpos, lend;
-                    const bool tst = active & leaf_open(lb, w0, w1, r.o, r.d, r.ix, r.iy, r.iz, r.best, lpos, lend);
-                    lpos = uni(lpos);
-                    lend = uni(lend);
+                    const uint32_t lpos = w0 & 0x3FFFFFFFu, lend = lpos + w1;
                     if constexpr (COUNT) c.leaf += active ? 1u : 0u;
-                    if (!__ballot(tst)) lend = lpos;
                     for (uint32_t i = lpos; i < lend; i += 2u) {
                         const bool two = lend - i >= 2u;
                         const uint32_t k0 = leafs[i], k1n = leafs[i + 1u];
@@ -789,7 +781,7 @@ __global__ void __launch_bounds__(BLOCK, 1) wf_extend_primary(const KernelParams
                         const float4 a0 = ld_tri<true>(tris + k0), a1 = ld_tri<true>(tris + k0 + 1);
                         const float4 a2 = ld_tri<true>(tris + k0 + 2), b0 = ld_tri<true>(tris + k1);
                         const float4 b1 = ld_tri<true>(tris + k1 + 1), b2 = ld_tri<true>(tris + k1 + 2);
-                        if (tst) {
+                        if (active) {
                             test_tri_pair(r, a0, a1, a2, k0, b0, b1, b2, k1, two);
                             if constexpr (COUNT) {
                                 c.refs += two ? 2u : 1u;

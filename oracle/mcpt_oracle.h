@@ -68,12 +68,8 @@ typedef struct {
                                        0: no tint (rtx.hlsl:345, the published renders) */
     int32_t mode;                   /* 0: CVMCTracer semantics; 1: QuinEngine (rtx.hlsl:304-405) */
     float proj11, proj22;           /* QE: PerspectiveFovRH scales (orc_qe_proj)  */
-    int32_t node_boxes;             /* ordered KD, the kernel's culls by image layout:
-                                        1: skip children whose fp16 KD box the ray misses (scenes
-                                           in global memory, 48-B pair records);
-                                        0: skip a reached leaf whose box (packed in its leaf word)
-                                           the ray misses (scenes in LDS, 8-B node words);
-                                       -1: no cull (the plain ordered walk) */
+    int32_t node_boxes;             /* ordered KD: skip children whose fp16 KD box the ray
+                                       misses (the kernel does for scenes in global memory) */
 } orc_params;
 
 typedef struct {

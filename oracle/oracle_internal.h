@@ -55,10 +55,6 @@ struct orc_scene {
     orc_node* nodes; int nnodes;
     uint32_t* leaf_ids; int nleaf_ids;
     int kd_depth;
-    /* leaf boxes of the 8-B node image (render_ref.c orc_build_leafboxes, csrc/leaf_box.hpp) */
-    uint32_t lb_qb;                 /* box bits per coordinate, 0: no leaf-box cull */
-    float lb_lo[3], lb_sc[3];
-    float* lbox;                    /* per node: the stored box, decoded (lo3 hi3) */
 };
 
 int orc_model_read(orc_model* m, const char* path, char* err, int errlen);
@@ -66,6 +62,5 @@ int orc_model_read_tinyobj(orc_model* m, const char* path, char* err, int errlen
 void orc_model_free(orc_model* m);
 /* KD build over kd triangles (vertex triples), flattened BFS */
 void orc_kd_build(orc_scene* s);
-void orc_build_leafboxes(orc_scene* s);
 
 #endif

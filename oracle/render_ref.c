@@ -479,78 +479,6 @@ static int box_hit(const orc_node* nd, const float* oo, const float* dd, const f
     return !out && !(lo * KD_EPS_LO > hi * KD_EPS_HI);
 }
 
-/* ====== leaf boxes in the leaf words of 8-B node images (kernel mirror) =====
- * csrc/leaf_box.hpp: rb = bits of the ref count, cb = bits of the largest leaf
- * count, qb = min(8, (30 - rb - cb) / 2) box bits per coordinate (none if
- * rb + cb > 22); codes on a grid over the root box, coordinate =
- * fmaf(code, sc[a], lo[a]), min corner rounded down, max corner up.  The walk
- * tests (0, best] against a leaf's box when it reaches the leaf (node_boxes 0,
- * the layout the kernel reads from LDS) and skips its triangles on a miss. */
-static uint32_t bitlen_u32(uint32_t x) { uint32_t n = 0; while (x) { n++; x >>= 1; } return n; }
-static float lb_dec(const orc_scene* s, int a, uint32_t q) { return fmaf((float)q, s->lb_sc[a], s->lb_lo[a]); }
-static uint32_t lb_code(const orc_scene* s, int a, float v, int dir) {
-    const int64_t mx = ((int64_t)1 << s->lb_qb) - 1;
-    if (!(s->lb_sc[a] > 0.0f)) return 0;
-    double x = ((double)v - s->lb_lo[a]) / s->lb_sc[a];
-    x = dir < 0 ? floor(x) : ceil(x);
-    int64_t q = x < 0 ? 0 : (x > (double)mx ? mx : (int64_t)x);
-    if (dir < 0) {
-        while (q > 0 && lb_dec(s, a, (uint32_t)q) > v) q--;
-        while (q < mx && lb_dec(s, a, (uint32_t)(q + 1)) <= v) q++;
-    } else {
-        while (q < mx && lb_dec(s, a, (uint32_t)q) < v) q++;
-        while (q > 0 && lb_dec(s, a, (uint32_t)(q - 1)) >= v) q--;
-    }
-    return (uint32_t)q;
-}
-void orc_build_leafboxes(orc_scene* s) {
-    free(s->lbox);
-    s->lbox = NULL;
-    s->lb_qb = 0;
-    if (!s->nnodes) return;
-    uint32_t maxc = 0;
-    for (int n = 0; n < s->nnodes; n++)
-        if (!s->nodes[n].axis && s->nodes[n].tri_count > maxc) maxc = s->nodes[n].tri_count;
-    const uint32_t rb = bitlen_u32((uint32_t)s->nleaf_ids), cb = bitlen_u32(maxc);
-    if (rb + cb > 22) return;
-    const uint32_t qb = (30u - rb - cb) / 2u;
-    s->lb_qb = qb > 8u ? 8u : qb;
-    const float mq = (float)((1u << s->lb_qb) - 1u);
-    for (int a = 0; a < 3; a++) {
-        const float lo = s->nodes[0].bmin[a], hi = s->nodes[0].bmax[a];
-        float sc = (hi - lo) / mq;
-        if (!(sc > 0.0f)) sc = 0.0f;
-        while (sc > 0.0f && fmaf(mq, sc, lo) < hi) sc = nextafterf(sc, INFINITY);
-        s->lb_lo[a] = lo;
-        s->lb_sc[a] = sc;
-    }
-    s->lbox = malloc(sizeof(float) * 6 * (size_t)s->nnodes);
-    for (int n = 0; n < s->nnodes; n++)
-        for (int a = 0; a < 3; a++) {
-            s->lbox[6 * n + a] = lb_dec(s, a, lb_code(s, a, s->nodes[n].bmin[a], -1));
-            s->lbox[6 * n + 3 + a] = lb_dec(s, a, lb_code(s, a, s->nodes[n].bmax[a], +1));
-        }
-}
-/* does (0, best] meet the leaf's stored box?  (trace_device.hpp leaf_open) */
-static int leaf_box_hit(const orc_scene* s, uint32_t node, const float* oo, const float* dd, const float* inv,
-                        float best) {
-    if (!s->lb_qb) return 1;
-    const float* b = s->lbox + 6 * (size_t)node;
-    float lo = 0.0f, hi = best;
-    int out = 0;
-    for (int a = 0; a < 3; a++) {
-        if (dd[a] == 0.0f) {
-            out |= (oo[a] < b[a]) | (oo[a] > b[3 + a]);
-        } else {
-            float t0 = (b[a] - oo[a]) * inv[a], t1 = (b[3 + a] - oo[a]) * inv[a];
-            float a0 = t0 < t1 ? t0 : t1, a1 = t0 < t1 ? t1 : t0;
-            lo = a0 > lo ? a0 : lo;
-            hi = a1 < hi ? a1 : hi;
-        }
-    }
-    return !out && !(lo * KD_EPS_LO > hi * KD_EPS_HI);
-}
-
 static hit_t isect_kd_ordered(qctx* q, orc_v3 o, orc_v3 d) {
     const orc_scene* s = q->s;
     hit_t h;
@@ -591,7 +519,7 @@ static hit_t isect_kd_ordered(qctx* q, orc_v3 o, orc_v3 d) {
             uint32_t farc = below ? nd->right : nd->left;
             /* child-box cull (scenes the kernel serves from global memory) */
             int nhit = 1, fhit = 1;
-            if (q->node_boxes == 1) {
+            if (q->node_boxes) {
                 nhit = box_hit(&s->nodes[nearc], oo, dd, inv, best);
                 fhit = box_hit(&s->nodes[farc], oo, dd, inv, best);
             }
@@ -617,9 +545,7 @@ static hit_t isect_kd_ordered(qctx* q, orc_v3 o, orc_v3 d) {
             nd = &s->nodes[node];
         }
         q->c.leaf_visits++;
-        /* node_boxes 0 (the LDS layout): the leaf-box cull */
-        const int leaf_in = q->node_boxes != 0 || leaf_box_hit(s, node, oo, dd, inv, best);
-        for (uint32_t i = 0; leaf_in && i < nd->tri_count; i++) {
+        for (uint32_t i = 0; i < nd->tri_count; i++) {
             uint32_t k = s->leaf_ids[nd->tri_begin + i];
             q->c.leaf_refs++;
             q->c.tri_tests++;
@@ -1067,14 +993,13 @@ orc_scene* orc_scene_load_ex(const char* path, int flavor, char* err, int errlen
         free(cv2kd);
     }
     orc_kd_build(s);
-    orc_build_leafboxes(s);
     return s;
 }
 
 void orc_scene_free(orc_scene* s) {
     if (!s) return;
     orc_model_free(&s->model);
-    free(s->geoms); free(s->tri_geom); free(s->kd_tris); free(s->kd_prio); free(s->nodes); free(s->leaf_ids); free(s->lbox);
+    free(s->geoms); free(s->tri_geom); free(s->kd_tris); free(s->kd_prio); free(s->nodes); free(s->leaf_ids);
     free(s);
 }
 

@@ -100,8 +100,7 @@ def test_ordered_walk_and_box_cull_equal_brute_force(oscene, oracle_mod, name):
     tb, gb, hb, cb = s.intersect(o, d, oracle_mod.BRUTE, threads=THREADS)
     assert 0.3 < (tb >= 0).mean() < 1.0
     kv = s.kd_verts()
-    # the plain ordered walk, with the leaf-box cull (LDS layout), with the child-box cull (global layout)
-    modes = [(oracle_mod.KD_ORDERED, -1), (oracle_mod.KD_ORDERED, 0), (oracle_mod.KD_ORDERED, 1)]
+    modes = [(oracle_mod.KD_ORDERED, 0), (oracle_mod.KD_ORDERED, 1)]
     for mode, boxes in modes:
         tk, gk, hk, ck = s.intersect(o, d, mode, node_boxes=boxes, threads=THREADS)
         bad = np.nonzero((tb != tk) | (gb != gk) | (hb.view(np.uint32) != hk.view(np.uint32)).any(axis=1))[0]
@@ -111,7 +110,7 @@ def test_ordered_walk_and_box_cull_equal_brute_force(oscene, oracle_mod, name):
             assert _float_artifact(kv, o[i], d[i], tb[i], hb[i], tk[i], hk[i]), (name, boxes, i, tb[i], tk[i])
         assert ck["tri_tests"] < 0.05 * cb["tri_tests"]
     # the cull is what prunes: fewer inner visits and triangle tests than the plain walk
-    _, _, _, c0 = s.intersect(o[:20000], d[:20000], oracle_mod.KD_ORDERED, node_boxes=-1, threads=THREADS)
+    _, _, _, c0 = s.intersect(o[:20000], d[:20000], oracle_mod.KD_ORDERED, node_boxes=0, threads=THREADS)
     _, _, _, c1 = s.intersect(o[:20000], d[:20000], oracle_mod.KD_ORDERED, node_boxes=1, threads=THREADS)
     assert c1["tri_tests"] <= c0["tri_tests"] and c1["inner_visits"] <= c0["inner_visits"]
 

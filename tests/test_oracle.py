@@ -282,7 +282,7 @@ def test_child_box_cull_is_exact_and_prunes(oracle_mod, mcpt):
     for name, sid in (("scene01", 1), ("scene02", 2), ("scene03", 2)):
         s = oracle_mod.Scene(mcpt.scene_path(name))
         kw = dict(width=40, height=30, spp=3, threads=8, scene_id=sid, traversal=oracle_mod.KD_ORDERED)
-        a, ca = s.render(oracle_mod.RenderParams(node_boxes=-1, **kw))
+        a, ca = s.render(oracle_mod.RenderParams(node_boxes=0, **kw))
         b, cb = s.render(oracle_mod.RenderParams(node_boxes=1, **kw))
         assert np.array_equal(a, b), name
         assert ca["rays"] == cb["rays"] and ca["shades"] == cb["shades"]
@@ -290,24 +290,6 @@ def test_child_box_cull_is_exact_and_prunes(oracle_mod, mcpt):
         if name != "scene03":   # scene03 from camera 2: few leaves, all of them hit
             assert cb["inner_visits"] < 0.8 * ca["inner_visits"], (name, ca["inner_visits"], cb["inner_visits"])
             assert cb["tri_tests"] < 0.5 * ca["tri_tests"], (name, ca["tri_tests"], cb["tri_tests"])
-
-
-def test_leaf_box_cull_is_exact_and_prunes(oracle_mod, mcpt):
-    """The leaf-box cull the kernel applies to scenes in LDS (leaf boxes packed
-    into the 8-B leaf words, csrc/leaf_box.hpp): identical images and equal
-    inner / leaf visit counts with it on (node_boxes 0) and off (-1); scene01's
-    triangle tests drop by more than half."""
-    for name, sid in (("scene01", 1), ("scene02", 2), ("scene03", 2)):
-        s = oracle_mod.Scene(mcpt.scene_path(name))
-        kw = dict(width=40, height=30, spp=3, threads=8, scene_id=sid, traversal=oracle_mod.KD_ORDERED)
-        a, ca = s.render(oracle_mod.RenderParams(node_boxes=-1, **kw))
-        b, cb = s.render(oracle_mod.RenderParams(node_boxes=0, **kw))
-        assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), name
-        for k in ("rays", "shades", "inner_visits", "leaf_visits"):
-            assert ca[k] == cb[k], (name, k)
-        assert cb["tri_tests"] <= ca["tri_tests"]
-        if name == "scene01":
-            assert cb["tri_tests"] < 0.5 * ca["tri_tests"], (ca["tri_tests"], cb["tri_tests"])
 
 
 def test_fp16_box_rounding_contains_and_matches_product(oracle_mod, tmp_path):
