@@ -268,12 +268,7 @@ void order_leaves(const mcpt::HostScene& hs, DeviceOrder& d) {
         }
 }
 
-#ifndef MCPT_CLUSTER_ALIGN
-#define MCPT_CLUSTER_ALIGN 0
-#endif
-// align: every cluster starts at a pair index that is a multiple of `align`
-// (48-B records, align 8: each 7-pair cluster in three whole 128-B lines)
-DeviceOrder device_order(const mcpt::HostScene& hs, uint32_t align = 1) {
+DeviceOrder device_order(const mcpt::HostScene& hs) {
     const uint32_t nn = static_cast<uint32_t>(hs.nodes.size());
     DeviceOrder d;
     d.node_new.assign(nn, 0xFFFFFFFFu);
@@ -296,7 +291,6 @@ DeviceOrder device_order(const mcpt::HostScene& hs, uint32_t align = 1) {
         for (uint32_t n : frontier)
             if (hs.nodes[n].axis) queue.push_back(n);
         if (list.empty()) continue;
-        if (align > 1) pairs = (pairs + align - 1) / align * align;
         for (uint32_t L : list) {
             d.node_new[L] = 2 * pairs + 1;
             d.node_new[L + 1] = 2 * pairs + 2;
@@ -343,7 +337,6 @@ void build_image(mcpt_scene& s, bool force_global) {
     if (mcpt::lds_bytes_in_lds(static_cast<uint32_t>(std::min<size_t>(total, 0xFFFFFFF0u)), 4) + 32 > mcpt::kMaxLds ||
         force_global) {
         boxes = true;
-        if (MCPT_CLUSTER_ALIGN) ord = device_order(hs, MCPT_CLUSTER_ALIGN);
         total = image_size(ord, off_nodes, off_leafs, off_geoms);
     }
     const size_t off_tris = 0;
