@@ -23,7 +23,8 @@ kernel's measured HBM traffic and rate under roofline.kernels (the queue
 streams: SURVEY 8(f)1), and every N = 1 run measures a 1 GiB device copy as
 the roofline's second denominator (roofline.peak_copy_measured).  cpu_baseline = BASELINE
 configs[0] (C1: 512x512, 16 spp, whole frame, one thread) on the CPU oracle,
-plus the same oracle on all of this process's cores over crops of the workload.
+plus the same oracle on all of this process's cores over whole frames of the
+workload at a few samples per pixel.
 
 Launch:  python bench.py [--gpus 1 --steps 3 --warmup 1]
          python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
@@ -304,31 +305,40 @@ def cpu_c1(gpu_rays: int) -> dict:
 
 def cpu_all_cores(scene_name: str, width: int, height: int, seconds: float, threads: int) -> dict:
     """The same oracle on `threads` host cores over a bounded sample of the GPU
-    workload: centred crops rendered until `seconds` pass."""
+    workload: whole frames (every pixel) at a few samples each, successive
+    passes continuing the sample sequence, until `seconds` pass (one thread:
+    centred crops, a whole pass would take minutes)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # test/bench infrastructure only
     from montecarlopathtracer_amd.scenes import scene_path
     oracle.build()
     s = oracle.Scene(scene_path(scene_name))
-    crop = 64 if threads == 1 else 256
-    spp = 8
+    whole = threads > 1
+    crop = 64
+    spp = 1 if whole else 8
     total_rays, total_paths, total_t = 0, 0, 0.0
     runs = 0
     while total_t < seconds and runs < 1024:
-        x0 = (width - crop) // 2 + (runs % 4) * 8
-        y0 = (height - crop) // 2 + (runs // 4 % 4) * 8
+        if whole:
+            region = (0, 0, width, height)
+        else:
+            x0 = (width - crop) // 2 + (runs % 4) * 8
+            y0 = (height - crop) // 2 + (runs // 4 % 4) * 8
+            region = (x0, y0, x0 + crop, y0 + crop)
         p = oracle.RenderParams(width=width, height=height, spp=spp, spp_chunk=32, spp_offset=runs * spp,
-                                traversal=oracle.KD_REF, threads=threads, region=(x0, y0, x0 + crop, y0 + crop))
+                                traversal=oracle.KD_REF, threads=threads, region=region)
         t0 = time.perf_counter()
         _, c = s.render(p)
         total_t += time.perf_counter() - t0
         total_rays += c["rays"]
         total_paths += c["paths"]
         runs += 1
+    what = (f"{runs} whole-frame pass(es) of {spp} spp (samples {0}..{runs * spp - 1})" if whole else
+            f"{runs} x ({crop}x{crop} centred crop, {spp} spp)")
     return {"value": round(total_rays / total_t / 1e6, 4), "unit": "Mray/s", "cores": threads,
             "mpath_s": round(total_paths / total_t / 1e6, 4),
-            "sample": f"{runs} x ({crop}x{crop} centred crop, {spp} spp) of {scene_name} {width}x{height}, "
-                      f"{total_rays} rays in {total_t:.1f}s, {threads} thread(s)"}
+            "sample": f"{what} of {scene_name} {width}x{height}, {total_rays} rays in {total_t:.1f}s, "
+                      f"{threads} thread(s)"}
 
 
 def cpu_baseline(scene_name: str, width: int, height: int, seconds: float, threads: int, gpu_c1_rays: int) -> dict:
