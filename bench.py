@@ -703,8 +703,8 @@ def main():
                                "own_layout_GBps": round(ab["own"] / (kern_ms * 1e-3) / 1e9, 1),
                                "per_ray": {k: round(per_launch[k] / max(per_launch["rays"], 1), 3) for k in
                                            ("inner_visits", "leaf_visits", "leaf_refs", "tri_tests", "shades")}}
-        sched = {k: plan[k] for k in ("wf_streams", "wf_batch", "wf_refill", "wf_group_shift") if
-                 args.pipeline == "wavefront"} if args.pipeline == "wavefront" else \
+        sched = {k: plan[k] for k in ("wf_streams", "wf_batch", "wf_batch_default", "wf_refill", "wf_group_shift")
+                 if args.pipeline == "wavefront"} if args.pipeline == "wavefront" else \
             {k: plan[k] for k in ("ready_thresh", "tail_units")}
         sched["workspace_GB"] = round(plan["workspace_bytes"] / 1e9, 2)
         if n_gpus > 1:

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define MCPT_ABI_VERSION 7
+#define MCPT_ABI_VERSION 8
 
 enum {
     MCPT_OK = 0,
@@ -189,6 +189,9 @@ typedef struct {
     uint64_t device_free_bytes; /* free memory of the scene's device now */
     int32_t devices;            /* devices the render runs on */
     int32_t peer_access;        /* multi-device: 1 if peer access between every pair is enabled */
+    uint32_t wf_batch_default;  /* wavefront: the batch the schedule picks with memory unbounded;
+                                   wf_batch below it = the queues were shrunk to fit (wf_mem_limit,
+                                   the scene's reservation or free device memory) -- ABI 8 */
 } mcpt_plan_info;
 
 /* Scene creation options (mcpt_scene_create_ex). */

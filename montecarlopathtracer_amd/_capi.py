@@ -21,7 +21,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MCPT_LIB_PATH") or os.path.join(_HERE, "lib", "libmcpt.so")
 
 MCPT_OK = 0
-ABI_VERSION = 7
+ABI_VERSION = 8
 MODE_CVMCTRACER = 0
 MODE_QUINENGINE = 1
 PIPELINE_MEGAKERNEL = 0
@@ -79,7 +79,8 @@ class PlanInfo(C.Structure):
     _fields_ = [("pipeline", C.c_int32), ("variant", C.c_int32), ("wf_streams", C.c_int32), ("wf_batch", C.c_uint32),
                 ("wf_refill", C.c_int32), ("wf_group_shift", C.c_int32), ("ready_thresh", C.c_int32),
                 ("tail_units", C.c_int32), ("work_paths", C.c_uint64), ("workspace_bytes", C.c_uint64), ("wf_queue_bytes", C.c_uint64),
-                ("device_free_bytes", C.c_uint64), ("devices", C.c_int32), ("peer_access", C.c_int32)]
+                ("device_free_bytes", C.c_uint64), ("devices", C.c_int32), ("peer_access", C.c_int32),
+                ("wf_batch_default", C.c_uint32)]
 
     def as_dict(self):
         return {n: int(getattr(self, n)) for n, _ in self._fields_}

@@ -1518,6 +1518,7 @@ int mcpt_plan_query(mcpt_scene* s, const mcpt_render_params* p, mcpt_plan_info* 
         }
         set_device(*s);
         Plan pl = make_plan(*s, &q);
+        const uint32_t unfitted = pl.wf_capacity;
         fit_wavefront(*s, pl);
         mcpt_plan_info r;
         std::memset(&r, 0, sizeof r);
@@ -1529,6 +1530,7 @@ int mcpt_plan_query(mcpt_scene* s, const mcpt_render_params* p, mcpt_plan_info* 
         else r.variant = mcpt::lds_bytes_in_lds(img, 8) <= mcpt::kMaxLds ? 1 : (mcpt::lds_bytes_in_lds(img, 4) <= mcpt::kMaxLds ? 2 : 3);
         r.wf_streams = wf ? pl.wf_streams : 0;
         r.wf_batch = wf ? pl.wf_capacity : 0;
+        r.wf_batch_default = wf ? unfitted : 0;
         r.wf_refill = wf ? pl.wf_refill : 0;
         r.wf_group_shift = wf ? static_cast<int32_t>(pl.wf_group_shift) : 0;
         r.ready_thresh = wf ? 0 : pl.kp.ready_thresh;

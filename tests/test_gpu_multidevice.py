@@ -163,6 +163,7 @@ def test_plan_query_reports_the_schedule(mcpt, devices):
     # queue order: 2 queues x (3 x 16 + 4 B) + 16 B of radiance = 120 B per path and stream
     assert 3 * 120 * (1 << 27) <= wf["wf_queue_bytes"] < 3 * 121 * (1 << 27) + (1 << 24)
     assert wf["wf_queue_bytes"] <= wf["workspace_bytes"] < wf["device_free_bytes"]
+    assert wf["wf_batch_default"] == wf["wf_batch"]          # nothing shrunk on an empty device
     srt = scene.plan(mcpt.RenderParams(pipeline="wavefront", wf_sort=True, **c2))
     assert 3 * 160 * (1 << 27) <= srt["wf_queue_bytes"] < 3 * 161 * (1 << 27) + (1 << 24)
     mk = scene.plan(mcpt.RenderParams(**c2))
@@ -186,6 +187,8 @@ def test_wavefront_memory_budget(mcpt):
     lim = big["wf_queue_bytes"] // 2
     small = scene.plan(mcpt.RenderParams(wf_mem_limit=lim, **kw))
     assert small["wf_batch"] < big["wf_batch"]
+    # the caller is told: the batch it would have had with memory unbounded
+    assert small["wf_batch_default"] == big["wf_batch"] == big["wf_batch_default"]
     img, st = scene.render(mcpt.RenderParams(wf_mem_limit=lim, **kw))
     assert np.array_equal(img, ref) and st["rays"] == rs["rays"]
     with pytest.raises(mcpt.McptError) as e:
