@@ -19,14 +19,16 @@ LIB = os.path.join(LIBDIR, os.environ.get("MCPT_LIB_NAME", "libmcpt.so"))
 SOURCES = ["host_model.cpp", "kd_cache.cpp", "capi.cpp", "render.hip", "wavefront.hip", "wavefront_primary.hip"]
 # per-source code generation (wavefront_primary.hip: the bounce-0 packet extend's
 # wave-uniform control flow as scalar branches; render.hip: GVN hoisting,
-# megakernel +1.4%, no effect on the wavefront kernels; the wavefront kernels:
+# megakernel +1.4%, no effect on the wavefront kernels, and the global-memory
+# variants' capped descent unrolled (C4 megakernel +2.1%); the wavefront kernels:
 # wave priority raised around their vector-memory loads, C2 +0.4%, and
-# if-diamonds of up to 8 instructions folded into selects -- only the
-# global-memory extends change, C4 +0.9%)
-_WF_FLAGS = ["-mllvm", "-amdgpu-set-wave-priority=1", "-mllvm", "-two-entry-phi-node-folding-threshold=8"]
+# if-diamonds of up to 8 instructions folded into selects and the capped
+# descent unrolled -- only the global-memory extends change, C4 +0.9% and +3.0%)
+_WF_FLAGS = ["-mllvm", "-amdgpu-set-wave-priority=1", "-mllvm", "-two-entry-phi-node-folding-threshold=8",
+             "-mllvm", "-unroll-threshold=2000"]
 SOURCE_FLAGS = {"wavefront_primary.hip": ["-mllvm", "-structurizecfg-skip-uniform-regions=1"] + _WF_FLAGS,
                 "wavefront.hip": _WF_FLAGS,
-                "render.hip": ["-mllvm", "-enable-gvn-hoist"]}
+                "render.hip": ["-mllvm", "-enable-gvn-hoist", "-mllvm", "-unroll-threshold=2000"]}
 HEADERS = ["host_model.hpp", "mcpt_device.hpp", "render_launch.hpp", "trace_device.hpp", "half_box.hpp"]
 ARCH = os.environ.get("MCPT_OFFLOAD_ARCH", "gfx950")
 
