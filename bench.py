@@ -55,6 +55,14 @@ def algorithmic_bytes(st: dict, pixels: int) -> dict:
     return {"survey": survey, "own": own}
 
 
+def ray_stream_bytes(rays: float, paths: float, variant: int) -> float:
+    """Bytes of ray stream the extend reads per frame: later bounces read 32 B
+    per ray (origin + direction); bounce 0 reads 16 B per path (the direction,
+    the origin is the eye) -- nothing on the LDS wavefront (kernel variant 4),
+    whose bounce-0 packet extend computes the primary rays itself (MCPT_WF_GEN0)."""
+    return (0.0 if variant == 4 else 16.0) * paths + 32.0 * (rays - paths)
+
+
 def _workload_args(args, shard=(1, 0)) -> list:
     return ["--scene", args.scene, "--width", str(args.width), "--height", str(args.height), "--spp", str(args.spp),
             "--spp-chunk", str(args.spp_chunk), "--pipeline", args.pipeline, "--wf-batch", str(args.wf_batch),
@@ -627,11 +635,10 @@ def main():
                             timing="sum of the extend dispatches' durations in the PMC pass (kernels serialized)")
                 rr = ext.get("read_requests")
                 if rr:
-                    # the extend's ray stream (bounce 0 reads 16 B per path: the direction, the origin is the
-                    # eye; later bounces 32 B: origin + direction) against the exact fabric reads: the rest
+                    # the extend's ray stream (ray_stream_bytes) against the exact fabric reads: the rest
                     # is node / triangle records (and stack refills) fetched past the L2
                     shard_rays, shard_paths = per_launch["rays"] / n_gpus, per_launch["paths"] / n_gpus
-                    ray_gb = (16.0 * shard_paths + 32.0 * (shard_rays - shard_paths)) / 1e9
+                    ray_gb = ray_stream_bytes(shard_rays, shard_paths, st["variant"]) / 1e9
                     roof["read_split"] = {
                         "exact_read_GB": rr["exact_read_GB"], "fetch_size_factor": rr["fetch_size_factor"],
                         "ray_GB": round(ray_gb, 3), "record_GB": round(rr["exact_read_GB"] - ray_gb, 3),
@@ -639,7 +646,8 @@ def main():
                         "spill_write_GB": round(16.0 * per_launch["stack_spills"] / n_gpus / 1e9, 3),
                         "method": "TCC_EA0_RDREQ_{32B,64B,128B} pass: exact = 32 n32 + 64 n64 + 128 n128 (every "
                                   "request 128 B here; FETCH_SIZE counts 64 B each, factor 2 exactly, "
-                                  "scripts/fetch_calib.hip); ray_GB from the counted rays / paths"}
+                                  "scripts/fetch_calib.hip); ray_GB from the counted rays / paths "
+                                  "(bench.ray_stream_bytes)"}
                 vb = valu_block(ext.pop("valu_counters", {}), cus, ext.get("ms", 0.0), per_launch["rays"] / n_gpus)
                 if vb:
                     vb["kernel"] = "wf_extend (the traversal: the dominant kernel), run alone"

@@ -43,7 +43,7 @@ def main(d, line=None, cus=256, extra=None):
         if "exact_read_GB" in out:
             rays = ln["rays_per_step"] / ln["n_gpus"]
             paths = ln["paths_per_step"] / ln["n_gpus"]
-            ray_gb = (16.0 * paths + 32.0 * (rays - paths)) / 1e9
+            ray_gb = b.ray_stream_bytes(rays, paths, ln["config"].get("kernel_variant")) / 1e9
             out["ray_GB"], out["record_GB"] = round(ray_gb, 3), round(out["exact_read_GB"] - ray_gb, 3)
         out["bench_line"] = {"achieved": r["achieved"], "frac": r["frac"], "traffic": r["traffic"],
                              "read_split": r.get("read_split")}
