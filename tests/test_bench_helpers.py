@@ -86,3 +86,12 @@ def test_lds_block_and_binding_roof():
     assert set(bd["fracs"]) == {"hbm", "lds_array", "valu_issue"}
     assert b.binding_of({"frac": 0.9, "lds": lb})["binding"] == "hbm"
     assert b.lds_block({}, cus, per) == {}
+
+
+def test_ray_stream_bytes():
+    """bench.ray_stream_bytes: 32 B per secondary ray; bounce 0 reads 16 B per
+    path except on the LDS wavefront (variant 4), whose packet extend computes
+    its primary rays."""
+    import bench
+    assert bench.ray_stream_bytes(10, 4, 5) == 16 * 4 + 32 * 6
+    assert bench.ray_stream_bytes(10, 4, 4) == 32 * 6
