@@ -41,7 +41,7 @@ def main(rec, probe=None):
     ln = load(rec)
     src = os.path.relpath(rec)
     print("| config | G rays/s | ms/frame | extend HBM frac | binding roof | VALU useful lanes | "
-          "record GB/frame past L2 | workspace GB | record |")
+          "reads past L2 beyond the ray stream, GB/frame | workspace GB | record |")
     print("|---|---|---|---|---|---|---|---|---|")
     print(row("C2 (1024², 1024 spp, wavefront)", ln, src))
     alt = ln.get("other_pipeline") or {}
