@@ -29,6 +29,8 @@ workload at a few samples per pixel.
 Launch:  python bench.py [--gpus 1 --steps 3 --warmup 1]
          python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
              --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
+         python bench.py --gpus N ...   (no launcher: starts the line above as a
+             child process; fewer than N visible GPUs exits non-zero)
 """
 from __future__ import annotations
 
@@ -55,19 +57,31 @@ def algorithmic_bytes(st: dict, pixels: int) -> dict:
     return {"survey": survey, "own": own}
 
 
-def ray_stream_bytes(rays: float, paths: float, variant: int) -> float:
-    """Bytes of ray stream the extend reads per frame: later bounces read 32 B
-    per ray (origin + direction); bounce 0 reads 16 B per path (the direction,
-    the origin is the eye) -- nothing on the LDS wavefront (kernel variant 4),
-    whose bounce-0 packet extend computes the primary rays itself (MCPT_WF_GEN0)."""
-    return (0.0 if variant == 4 else 16.0) * paths + 32.0 * (rays - paths)
+def ray_stream_bytes(rays: float, paths: float, variant: int, sort: bool = False, qe: bool = False) -> float:
+    """Bytes of ray stream the extend reads per frame (wavefront.hip implicit0 /
+    the packet bounce 0): later bounces read 32 B per ray (origin + direction).
+    Bounce 0 in CV mode with the queue-order shade reads 16 B per path (the
+    direction; the origin is the eye), and nothing on the LDS wavefront (kernel
+    variant 4), whose bounce-0 packet extend computes the primary rays itself
+    (MCPT_WF_GEN0); with the material sort or in QuinEngine mode (near-plane
+    origins) bounce 0 reads both streams, 32 B per path."""
+    implicit0 = not sort and not qe
+    b0 = (0.0 if variant == 4 else 16.0) if implicit0 else 32.0
+    return b0 * paths + 32.0 * (rays - paths)
+
+
+def hit_write_bytes(rays: float, sort: bool = False) -> float:
+    """The extend's hit stream: the 4-B triangle id per ray in queue order, the
+    16-B hit record {t, beta, gamma, id} under the material sort."""
+    return (16.0 if sort else 4.0) * rays
 
 
 def _workload_args(args, shard=(1, 0)) -> list:
     return ["--scene", args.scene, "--width", str(args.width), "--height", str(args.height), "--spp", str(args.spp),
             "--spp-chunk", str(args.spp_chunk), "--pipeline", args.pipeline, "--wf-batch", str(args.wf_batch),
             "--wf-streams", str(args.wf_streams), "--pmc-shard", f"{shard[0]},{shard[1]}", "--layout", args.layout] + \
-        [x for kv in args.set for x in ("--set", kv)] + (["--counting"] if args.counting else [])
+        [x for kv in args.set for x in ("--set", kv)] + (["--counting"] if args.counting else []) + \
+        (["--wf-sort"] if args.wf_sort else []) + ["--kd-build", args.kd_build]
 
 
 SCHED_FIELDS = ("wf_refill", "wf_group_shift", "ready_thresh", "tail_units_per_lane", "tail_units", "wf_mem_limit")
@@ -370,7 +384,7 @@ def host_cores() -> int:
     return max(1, min(n, int(os.environ.get("OMP_NUM_THREADS", "16"))))
 
 
-def child_line(args, scene: str, spp: int, steps: int, warmup: int, tag: str) -> dict:
+def child_line(args, scene: str, spp: int, steps: int, warmup: int, tag: str, extra: tuple = ()) -> dict:
     """Another BASELINE configuration timed the same way (same pipeline, PMC
     roofline passes) in a child process of this bench (its own GPU context;
     this process's workspace stays allocated beside it)."""
@@ -379,7 +393,7 @@ def child_line(args, scene: str, spp: int, steps: int, warmup: int, tag: str) ->
            "--no-cpu-baseline", "--steps", str(steps), "--warmup", str(warmup),
            "--width", str(args.width), "--height", str(args.height), "--spp", str(spp),
            "--spp-chunk", str(args.spp_chunk), "--pipeline", args.pipeline] + (["--no-pmc"] if args.no_pmc else []) + \
-        (["--keep-pmc", os.path.join(args.keep_pmc, tag)] if args.keep_pmc else [])
+        (["--keep-pmc", os.path.join(args.keep_pmc, tag)] if args.keep_pmc else []) + list(extra)
     env = dict(os.environ)
     for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
@@ -412,6 +426,53 @@ def c5_line(args) -> dict:
     return line
 
 
+def c2_sah_line(args) -> dict:
+    """The C2 workload on the opt-in SAH KD tree (mcpt_scene_options::kd_build
+    = SAH): the same image bit for bit (tests/test_gpu_sah_tree.py), fewer
+    node visits.  Not the headline -- the north star keeps the reference's
+    KDTree build -- but what a user may switch to.  Same steps, PMC passes."""
+    line = child_line(args, "scene01", args.spp, args.steps, args.warmup, "c2_sah", extra=("--kd-build", "sah"))
+    return line
+
+
+def c5_sorted_line(args) -> dict:
+    """BASELINE configs[4] as it is worded -- per-bounce compaction PLUS the
+    material sort (wf_sort = 1: extend appends each hit to its material's class
+    list, shade reads the classes in turn) -- on one GPU, 3 steps, no PMC
+    passes (the same image as the c5 line, bit for bit)."""
+    line = child_line(args, "scene01", 4 * args.spp, 3, 1, "c5_sorted", extra=("--wf-sort", "--no-pmc"))
+    if "config" in line:
+        line["config"]["shade"] = "material-sorted (wf_sort=1: per-bounce compaction + class lists)"
+    return line
+
+
+def launch_ranks(args, argv: list) -> int:
+    """`--gpus N > 1` started without a launcher (no WORLD_SIZE): run N ranks
+    as the driver would -- `torch.distributed.run --nproc-per-node N` on this
+    script, as a CHILD process started before this process touches the GPU
+    (torch.cuda.device_count() does not initialise it) -- and return its exit
+    code; its rank 0 prints the line.  Fewer than N visible GPUs is an error
+    (a one-GPU line labelled N GPUs would be unmeasured), except under the
+    MCPT_DIST_BACKEND=gloo rehearsal, whose ranks share the GPUs there are."""
+    import socket
+    import subprocess
+    import torch
+    n = args.gpus
+    have = torch.cuda.device_count()
+    if os.environ.get("MCPT_DIST_BACKEND", "nccl") == "nccl" and have < n:
+        print(f"bench.py: --gpus {n} but {have} GPU(s) visible; refusing to report a {have}-GPU run as {n}",
+              file=sys.stderr, flush=True)
+        return 2
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + argv
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -431,6 +492,13 @@ def main():
     ap.add_argument("--no-alt", action="store_true", help="skip the other pipeline's comparison timing (N = 1)")
     ap.add_argument("--wf-batch", type=int, default=0)
     ap.add_argument("--wf-streams", type=int, default=0, help="wavefront streams (0 = the library's default)")
+    ap.add_argument("--kd-build", choices=["reference", "sah"], default="reference",
+                    help="KD split rule (mcpt_scene_options::kd_build): the reference's KDTree.hpp rule (the "
+                         "headline) or the opt-in SAH with a traversal cost (same image, fewer node visits)")
+    ap.add_argument("--no-sah", action="store_true",
+                    help="N = 1: skip the C2 line on the SAH tree reported under extra_lines.c2_sah_tree")
+    ap.add_argument("--wf-sort", action="store_true",
+                    help="wavefront: the material-sorted shade (mcpt_render_params::wf_sort = 1; same image)")
     ap.add_argument("--single-process", action="store_true",
                     help="one process drives all --gpus devices through mcpt_init(devices) (the C ABI's "
                          "multi-device render: replicas, peer-copy gather) instead of one rank per GPU")
@@ -461,13 +529,20 @@ def main():
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)   # one render under rocprofv3
     args = ap.parse_args()
     if args.no_extra:
-        args.no_c4 = args.no_c5 = True
+        args.no_c4 = args.no_c5 = args.no_sah = True
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ and not args.single_process and not args.pmc_child:
+        sys.exit(launch_ranks(args, sys.argv[1:]))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if not args.pmc_child and not args.single_process and world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} ranks were launched")
 
+    import datetime
     import torch
     import torch.distributed as dist
     import montecarlopathtracer_amd as M
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # MCPT_DIST_BACKEND=gloo: rehearsal of the N > 1 path with every rank on the
@@ -477,12 +552,17 @@ def main():
     if world > 1 and args.single_process:
         raise SystemExit("--single-process drives every GPU from one process: launch it without torch.distributed.run")
     if world > 1:
+        if backend == "nccl" and local >= torch.cuda.device_count():
+            raise SystemExit(f"bench.py: rank {rank} (local {local}) has no GPU: "
+                             f"{torch.cuda.device_count()} visible for {world} ranks")
         local = local % max(torch.cuda.device_count(), 1) if backend == "gloo" else local
         torch.cuda.set_device(local)
+        # bounded: a stuck RCCL set-up exits non-zero inside the driver's limit
+        tmo = datetime.timedelta(seconds=int(os.environ.get("MCPT_DIST_TIMEOUT_S", "180")))
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=tmo)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=tmo)
     dev = torch.device("cuda", local if world > 1 else 0)
     red_dev = dev if backend == "nccl" else torch.device("cpu")   # device of the small timing reductions
     torch.cuda.set_device(dev)
@@ -496,15 +576,17 @@ def main():
                          f"{torch.cuda.device_count()} device(s) visible")
     M.Tracer().initialize(devices if n_dev > 1 else [dev.index])
     n_gpus = world * n_dev
+    if not args.pmc_child and n_gpus != args.gpus:    # never a line whose n_gpus is not --gpus
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but {n_gpus} GPU(s) would render")
 
-    scene = M.Scene(M.ObjModel(M.scene_path(args.scene)), layout=args.layout)
+    scene = M.Scene(M.ObjModel(M.scene_path(args.scene)), layout=args.layout, kd_build=args.kd_build)
     scene_id = 2 if args.scene in ("scene02", "scene03") else 1
     if args.pmc_child:   # PMC pass: exactly one render of the timed kernel (rank 0's shard), then exit
         sc, si = (int(x) for x in args.pmc_shard.split(","))
         p = M.RenderParams.for_scene(scene_id, width=args.width, height=args.height, spp=args.spp,
                                      spp_chunk=args.spp_chunk, tile=8, pipeline=args.pipeline, wf_batch=args.wf_batch,
                                      wf_streams=args.wf_streams, shard_count=sc, shard_index=si, packed=sc > 1,
-                                     lean=not args.counting, **_tuning(args))
+                                     lean=not args.counting, wf_sort=args.wf_sort, **_tuning(args))
         fb = torch.zeros((p.output_pixels(), 4), dtype=torch.float32, device=dev)
         scene.render_device(p, fb.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
         torch.cuda.synchronize(dev)
@@ -516,7 +598,8 @@ def main():
     p = M.RenderParams.for_scene(scene_id, width=args.width, height=args.height, spp=args.spp,
                                  spp_chunk=args.spp_chunk, tile=8, shard_count=world, shard_index=rank,
                                  packed=world > 1, pipeline=args.pipeline, wf_batch=args.wf_batch,
-                                 wf_streams=args.wf_streams, lean=lean, gather=args.gather, **_tuning(args))
+                                 wf_streams=args.wf_streams, lean=lean, gather=args.gather, wf_sort=args.wf_sort,
+                                 **_tuning(args))
     p_count = dataclasses.replace(p, lean=False)
     n_out = p.output_pixels()
     fb = torch.zeros((n_out, 4), dtype=torch.float32, device=dev)
@@ -609,7 +692,8 @@ def main():
         algo_gbs = ab["survey"] / (kern_ms * 1e-3) / 1e9
         mray = rays / elapsed / 1e6
         workload = f"cornell_{args.width}x{args.height}_{args.spp}spp" + ("" if args.scene == "scene01" else
-                                                                            f"_{args.scene}")
+                                                                            f"_{args.scene}") + \
+            ("" if args.kd_build == "reference" else f"_kd_{args.kd_build}")
         cus = torch.cuda.get_device_properties(dev).multi_processor_count
         # the PMC passes profile one device's share: rank 0's shard (N > 1) or the whole frame
         shard = (n_gpus, 0) if n_gpus > 1 else (1, 0)
@@ -638,11 +722,11 @@ def main():
                     # the extend's ray stream (ray_stream_bytes) against the exact fabric reads: the rest
                     # is node / triangle records (and stack refills) fetched past the L2
                     shard_rays, shard_paths = per_launch["rays"] / n_gpus, per_launch["paths"] / n_gpus
-                    ray_gb = ray_stream_bytes(shard_rays, shard_paths, st["variant"]) / 1e9
+                    ray_gb = ray_stream_bytes(shard_rays, shard_paths, st["variant"], sort=args.wf_sort) / 1e9
                     roof["read_split"] = {
                         "exact_read_GB": rr["exact_read_GB"], "fetch_size_factor": rr["fetch_size_factor"],
                         "ray_GB": round(ray_gb, 3), "record_GB": round(rr["exact_read_GB"] - ray_gb, 3),
-                        "hit_id_write_GB": round(4.0 * shard_rays / 1e9, 3),
+                        "hit_id_write_GB": round(hit_write_bytes(shard_rays, args.wf_sort) / 1e9, 3),
                         "spill_write_GB": round(16.0 * per_launch["stack_spills"] / n_gpus / 1e9, 3),
                         "method": "TCC_EA0_RDREQ_{32B,64B,128B} pass: exact = 32 n32 + 64 n64 + 128 n128 (every "
                                   "request 128 B here; FETCH_SIZE counts 64 B each, factor 2 exactly, "
@@ -729,6 +813,8 @@ def main():
             "config": {"workload": workload, "scene": args.scene,
                        "width": args.width, "height": args.height, "spp": args.spp, "max_depth": 7,
                        "spp_chunk": args.spp_chunk, "parallelism": par, "pipeline": args.pipeline,
+                       "wf_sort": bool(args.wf_sort), "kd_build": args.kd_build,
+                       "kd_nodes": scene.info()["n_nodes"],
                        "kernel_variant": st["variant"], "schedule": sched},
             "rays_per_step": rays // args.steps,
             "paths_per_step": st["paths"] // args.steps,
@@ -749,8 +835,11 @@ def main():
             extra = {}
             if not args.no_c4:
                 extra["c4"] = c4_line(args)
+            if not args.no_sah and args.kd_build == "reference":
+                extra["c2_sah_tree"] = c2_sah_line(args)
             if not args.no_c5 and args.spp == 1024 and args.pipeline == "wavefront":
                 extra["c5"] = c5_line(args)
+                extra["c5_sorted"] = c5_sorted_line(args)
             if extra:
                 line["extra_lines"] = extra
         if n_gpus == 1 and not args.no_cpu_baseline:

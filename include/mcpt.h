@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define MCPT_ABI_VERSION 8
+#define MCPT_ABI_VERSION 9
 
 enum {
     MCPT_OK = 0,
@@ -67,6 +67,7 @@ typedef struct {
     int64_t device;        /* HIP device ordinal holding the scene */
     int64_t node_boxes;    /* 1: served from global memory, children culled by their KD boxes */
     int64_t n_devices;     /* devices holding a replica (mcpt_init's list at creation); 0 host-only */
+    int64_t kd_build;      /* MCPT_KD_BUILD_* the tree was built with -- ABI 9 */
 } mcpt_scene_info;
 
 typedef struct {
@@ -199,11 +200,19 @@ typedef struct {
     const char* kd_cache_dir;   /* on-disk KD-build cache directory (must exist); NULL = none */
     int32_t host_only;          /* 1: no device allocation */
     int32_t layout;             /* MCPT_LAYOUT_*: scene image placement */
+    int32_t kd_build;           /* MCPT_KD_BUILD_*: the KD tree's split rule -- ABI 9 */
 } mcpt_scene_options;
 
 enum {
     MCPT_LAYOUT_AUTO = 0,       /* LDS image (8-B nodes) when it fits, else global memory with child boxes */
     MCPT_LAYOUT_GLOBAL = 1      /* global memory with 48-B child-box pair records, whatever the size */
+};
+/* KD split rule.  Images do not depend on it (the closest hit is the
+ * brute-force one for any tree); visit counts and speed do. */
+enum {
+    MCPT_KD_BUILD_REFERENCE = 0,  /* QuinEngine KDTree.hpp:58-287: median > 64 tris, SAH with Cts = 0 below */
+    MCPT_KD_BUILD_SAH = 1         /* SAH with a traversal cost over split-plane regions at every size
+                                     (empty space cut off): fewer node visits per ray (host_model.cpp) */
 };
 
 /* ---- library ------------------------------------------------------------ */
@@ -323,9 +332,16 @@ int mcpt_intersect(mcpt_scene* s, int64_t n, const float* o, const float* d, flo
  * (required before hipGraph capture).  Megakernel workspace per render:
  * partial sums 16 B x pixels x ceil(spp/chunk), the tail-split buffer (16 B
  * per sample of the last ~4 units per lane) and the stack spill area (32 x
- * 16 B per lane); wavefront: 120 B per path of the batch (160 with wf_sort).  */
+ * 16 B per lane); wavefront: 120 B per path of the batch (160 with wf_sort).
+ * After a reserve, a render on a CAPTURING stream that needs more than the
+ * scene holds fails with MCPT_E_NOMEM before any launch; a render on a
+ * non-capturing stream grows the workspace, and the buffers it outgrows are
+ * kept (not freed) until mcpt_scene_destroy, so a graph captured earlier
+ * stays valid.                                                               */
 int mcpt_scene_reserve(mcpt_scene* s, const mcpt_render_params* p);
-/* The scheduling a render of p would use and its memory (no allocation, no launch). */
+/* The scheduling a render of p would use and its memory (no allocation, no
+ * launch), for a render on a stream that is not capturing a graph (a
+ * captured render is held to the scene's reservation, mcpt_scene_reserve).  */
 int mcpt_plan_query(mcpt_scene* s, const mcpt_render_params* p, mcpt_plan_info* out);
 
 #ifdef __cplusplus

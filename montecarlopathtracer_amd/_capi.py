@@ -21,7 +21,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MCPT_LIB_PATH") or os.path.join(_HERE, "lib", "libmcpt.so")
 
 MCPT_OK = 0
-ABI_VERSION = 8
+ABI_VERSION = 9
 MODE_CVMCTRACER = 0
 MODE_QUINENGINE = 1
 PIPELINE_MEGAKERNEL = 0
@@ -45,7 +45,7 @@ class ModelInfo(C.Structure):
 class SceneInfo(C.Structure):
     _fields_ = [(n, C.c_int64) for n in
                 ("n_geometries", "n_triangles", "n_nodes", "n_leaf_refs", "kd_depth", "lds_bytes", "device",
-                 "node_boxes", "n_devices")]
+                 "node_boxes", "n_devices", "kd_build")]
 
 
 class RenderParamsC(C.Structure):
@@ -87,13 +87,16 @@ class PlanInfo(C.Structure):
 
 
 class SceneOptions(C.Structure):
-    _fields_ = [("kd_cache_dir", C.c_char_p), ("host_only", C.c_int32), ("layout", C.c_int32)]
+    _fields_ = [("kd_cache_dir", C.c_char_p), ("host_only", C.c_int32), ("layout", C.c_int32),
+                ("kd_build", C.c_int32)]
 
 
 OBJ_CVMCTRACER = 0
 OBJ_TINYOBJ = 1
 LAYOUT_AUTO = 0
 LAYOUT_GLOBAL = 1
+KD_BUILD_REFERENCE = 0
+KD_BUILD_SAH = 1
 
 
 class ModelDesc(C.Structure):

@@ -168,11 +168,21 @@ struct mcpt_scene {
     void* d_normals = nullptr;
     Workspace ws;
     std::vector<Timing> pending, free_timing;
+    // events of renders captured into a graph: recorded by the graph's replays,
+    // never read (a captured render has no time of its own) nor recycled
+    // (created once, mcpt_scene_reserve)
+    Timing capture_timing{};
+    bool has_capture_timing = false;
     int last_variant = 0;
     uint64_t renders = 0;
     // wavefront queue bytes set aside by mcpt_scene_reserve: later renders with a
     // default batch never grow past them (no hipMalloc inside a stream capture)
     size_t wf_reserved = 0;
+    // set by mcpt_scene_reserve: from then on a workspace buffer that has to grow
+    // is retired (kept until the scene is destroyed), never freed, so a HIP graph
+    // captured against the reservation keeps valid pointers (grow_ws)
+    bool reserved = false;
+    std::vector<void*> retired;
     // multi-device scene (mcpt_init with n > 1): the primary (this object, on
     // devices[0]) owns one replica per further device -- the same image and
     // normals, its own workspace, a non-blocking stream and a completion event --
@@ -210,8 +220,10 @@ struct mcpt_scene {
         }
         for (void* p : {d_image, d_normals, ws.partial, ws.small, ws.spill, ws.fb, ws.wf, ws.tail, gather, gather_send})
             if (p) (void)hipFree(p);
+        for (void* p : retired) (void)hipFree(p);
         for (auto& t : pending) for (auto ev : t.e) (void)hipEventDestroy(ev);
         for (auto& t : free_timing) for (auto ev : t.e) (void)hipEventDestroy(ev);
+        if (has_capture_timing) for (auto ev : capture_timing.e) (void)hipEventDestroy(ev);
         for (hipEvent_t ev : {done, start, wf_fork})
             if (ev) (void)hipEventDestroy(ev);
         for (int i = 0; i < mcpt::kMaxWfStreams; i++) {
@@ -433,9 +445,29 @@ void ensure_buf(void*& p, size_t& have, size_t need) {
     have = need;
 }
 
+// A workspace buffer of scene s grown to `need` bytes.  Once the scene has been
+// reserved (mcpt_scene_reserve), the old buffer is retired instead of freed --
+// a HIP graph captured against it keeps valid memory (its replays use the old
+// buffers, later renders the new ones) -- and on a capturing stream nothing is
+// allocated at all: a captured render that needs more than the scene holds
+// fails with MCPT_E_NOMEM before any launch (reserve for its params first).
+void grow_ws(mcpt_scene& s, void*& p, size_t& have, size_t need, bool capturing) {
+    if (have >= need && p) return;
+    if (capturing)
+        throw mcpt::Error{MCPT_E_NOMEM, "render needs more workspace than the scene holds while its stream is "
+                                        "capturing a graph: call mcpt_scene_reserve with these params first"};
+    if (p && s.reserved) {
+        s.retired.push_back(p);
+        p = nullptr;
+        have = 0;
+    }
+    ensure_buf(p, have, need);
+}
+
 struct Plan {
     mcpt::KernelParams kp;
     size_t out_pixels;
+    bool capturing = false;      // the render's stream is capturing a graph: nothing may be allocated
     int pipeline;
     int wf_streams;              // wavefront streams (wavefront_streams)
     uint32_t wf_capacity;        // paths per wavefront batch
@@ -638,7 +670,7 @@ bool stream_capturing(hipStream_t st) {
     HIP_TRY(hipStreamIsCapturing(st, &cs));
     return cs != hipStreamCaptureStatusNone;
 }
-void fit_wavefront(const mcpt_scene& s, Plan& pl, hipStream_t st = nullptr) {
+void fit_wavefront(const mcpt_scene& s, Plan& pl) {
     if (pl.pipeline != MCPT_PIPELINE_WAVEFRONT) return;
     uint64_t budget = pl.wf_mem_limit;
     bool reserved = false;
@@ -665,7 +697,7 @@ void fit_wavefront(const mcpt_scene& s, Plan& pl, hipStream_t st = nullptr) {
     };
     uint64_t cap = fit(reserved ? std::min<uint64_t>(budget, s.wf_reserved) : budget);
     if (reserved && need(cap) > s.wf_reserved) {
-        if (stream_capturing(st)) budget = std::min<uint64_t>(budget, s.wf_reserved);
+        if (pl.capturing) budget = std::min<uint64_t>(budget, s.wf_reserved);
         else cap = fit(budget);
     }
     if (need(cap) > budget) {
@@ -699,14 +731,14 @@ uint64_t tail_units_for(const mcpt_scene& s, const Plan& pl) {
 
 void prepare_workspace(mcpt_scene& s, Plan& pl, bool tail_split = false, int spill_sets = 1) {
     mcpt::KernelParams& k = pl.kp;
-    ensure_buf(s.ws.partial, s.ws.partial_bytes, size_t(k.nchunks) * k.npix_local * 16);
+    grow_ws(s, s.ws.partial, s.ws.partial_bytes, size_t(k.nchunks) * k.npix_local * 16, pl.capturing);
     if (!s.ws.small) {
         HIP_TRY(hipMalloc(&s.ws.small, 256));
         HIP_TRY(hipMemset(s.ws.small, 0, 256));
     }
     const size_t lanes = static_cast<size_t>(mcpt::total_lanes_for(s.gpu.image_bytes, s.cus));
     // (the wavefront's streams run extends concurrently: one spill area each)
-    ensure_buf(s.ws.spill, s.ws.spill_bytes, size_t(spill_sets) * 32 * lanes * 16);
+    grow_ws(s, s.ws.spill, s.ws.spill_bytes, size_t(spill_sets) * 32 * lanes * 16, pl.capturing);
     k.partial = static_cast<float4*>(s.ws.partial);
     k.counter = static_cast<uint32_t*>(s.ws.small);
     k.stats = reinterpret_cast<unsigned long long*>(static_cast<char*>(s.ws.small) + 64);
@@ -717,7 +749,7 @@ void prepare_workspace(mcpt_scene& s, Plan& pl, bool tail_split = false, int spi
     if (tail_split) {
         const uint64_t tail = tail_units_for(s, pl);
         if (tail) {
-            ensure_buf(s.ws.tail, s.ws.tail_bytes, size_t(tail) * k.chunk * 16);
+            grow_ws(s, s.ws.tail, s.ws.tail_bytes, size_t(tail) * k.chunk * 16, pl.capturing);
             k.tail_units = k.total_units - static_cast<uint32_t>(tail);
             k.total_items = k.tail_units + static_cast<uint32_t>(tail * k.chunk);
             k.tail_buf = static_cast<float4*>(s.ws.tail);
@@ -730,7 +762,11 @@ void prepare_workspace(mcpt_scene& s, Plan& pl, bool tail_split = false, int spi
 // per stream (`sets`: batches rotate over the wavefront's streams, each with its own)
 void prepare_wavefront(mcpt_scene& s, const Plan& pl, int sets, mcpt::WfParams* out) {
     const WfLayout l = wf_layout(s, pl, pl.wf_capacity);
-    ensure_buf(s.ws.wf, s.ws.wf_bytes, l.need * size_t(sets));
+    grow_ws(s, s.ws.wf, s.ws.wf_bytes, l.need * size_t(sets), pl.capturing);
+    // a default-batch render that grew the queues past the reservation: the
+    // grown queues are the reservation now (a later captured render of the same
+    // params allocates nothing and must not be refused)
+    if (s.reserved) s.wf_reserved = std::max(s.wf_reserved, s.ws.wf_bytes);
     for (int h = 0; h < sets; ++h) {
         char* b = static_cast<char*>(s.ws.wf) + size_t(h) * l.need;
         mcpt::WfParams& w = out[h];
@@ -775,6 +811,12 @@ bool multi_device(const mcpt_scene& s, const mcpt_render_params* p, const uint32
            !d_unit_counters;
 }
 
+void ensure_capture_timing(mcpt_scene& s) {
+    if (s.has_capture_timing) return;
+    for (auto& ev : s.capture_timing.e) HIP_TRY(hipEventCreate(&ev));
+    s.has_capture_timing = true;
+}
+
 void render_async(mcpt_scene& s, const mcpt_render_params* p, float* d_fb, hipStream_t st,
                   uint32_t* d_unit_counters = nullptr, bool raw_mean = false) {
     if (!s.on_device) throw mcpt::Error{MCPT_E_INVALID, "scene was created host-only"};
@@ -785,14 +827,18 @@ void render_async(mcpt_scene& s, const mcpt_render_params* p, float* d_fb, hipSt
     }
     set_device(s);
     Plan pl = make_plan(s, p);
-    fit_wavefront(s, pl, st);
+    pl.capturing = stream_capturing(st);
+    fit_wavefront(s, pl);
     pl.kp.raw_mean = raw_mean ? 1 : 0;
     // the tail split hands units out by sample, so per-unit counters need whole units
     const int wf_sets = pl.pipeline == MCPT_PIPELINE_WAVEFRONT ? pl.wf_streams : 1;
     prepare_workspace(s, pl, pl.pipeline == MCPT_PIPELINE_MEGAKERNEL && !d_unit_counters, wf_sets);
     pl.kp.unit_counters = d_unit_counters;
     Timing t;
-    if (!s.free_timing.empty()) {
+    if (pl.capturing) {
+        ensure_capture_timing(s);
+        t = s.capture_timing;
+    } else if (!s.free_timing.empty()) {
         t = s.free_timing.back();
         s.free_timing.pop_back();
     } else {
@@ -818,6 +864,7 @@ void render_async(mcpt_scene& s, const mcpt_render_params* p, float* d_fb, hipSt
         HIP_TRY(mcpt::launch_render(pl.kp, s.cus, st, t.e[0], t.e[1], t.e[2], reinterpret_cast<float4*>(d_fb),
                                     &s.last_variant));
     }
+    if (pl.capturing) return;   // timed and counted when replayed, not now
     s.pending.push_back(t);
     s.renders++;
 }
@@ -904,12 +951,13 @@ void render_multi(mcpt_scene& s, const mcpt_render_params* p, float* d_fb, hipSt
     const int T = full.kp.tile;
     const uint64_t slot = multi_slot(full, p, n);
     if (slot * n >= (uint64_t(1) << 32)) throw mcpt::Error{MCPT_E_UNSUPPORTED, "image too large"};
-    ensure_buf(s.gather, s.gather_bytes, size_t(n) * slot * 16);
+    const bool cap = stream_capturing(st);
+    grow_ws(s, s.gather, s.gather_bytes, size_t(n) * slot * 16, cap);
     if (use_rccl) {
         ensure_comms(s);
         // every rank sends `slot` pixels (ncclGather's equal counts; the shards'
         // own counts differ by at most one tile): rank 0 from gather_send
-        ensure_buf(s.gather_send, s.gather_send_bytes, size_t(slot) * 16);
+        grow_ws(s, s.gather_send, s.gather_send_bytes, size_t(slot) * 16, cap);
     }
     if (!s.start) HIP_TRY(hipEventCreateWithFlags(&s.start, hipEventDisableTiming));
     HIP_TRY(hipEventRecord(s.start, st));
@@ -925,7 +973,7 @@ void render_multi(mcpt_scene& s, const mcpt_render_params* p, float* d_fb, hipSt
         set_device(R);
         const mcpt_render_params pr = shard(r);
         const size_t bytes = size_t(mcpt_shard_pixel_count(&pr)) * 16;
-        ensure_buf(R.ws.fb, R.ws.fb_bytes, use_rccl ? size_t(slot) * 16 : bytes);
+        grow_ws(R, R.ws.fb, R.ws.fb_bytes, use_rccl ? size_t(slot) * 16 : bytes, cap);
         HIP_TRY(hipStreamWaitEvent(R.stream, s.start, 0));
         render_async(R, &pr, static_cast<float*>(R.ws.fb), R.stream, nullptr, true);
         if (use_rccl) continue;                        // gathered below, all ranks in one group
@@ -1227,12 +1275,15 @@ int mcpt_model_group(const mcpt_model* m, int64_t g, char* name_buf, int64_t nam
 }
 
 static int scene_create_impl(const mcpt_model* m, mcpt_scene** out, bool device, const char* kd_cache_dir = nullptr,
-                             int32_t* cache_hit = nullptr, int32_t layout = MCPT_LAYOUT_AUTO) {
+                             int32_t* cache_hit = nullptr, int32_t layout = MCPT_LAYOUT_AUTO,
+                             int32_t kd_build = MCPT_KD_BUILD_REFERENCE) {
     return guarded([&]() -> int {
         if (!m || !out) return fail(MCPT_E_INVALID, "NULL argument");
+        if (kd_build != MCPT_KD_BUILD_REFERENCE && kd_build != MCPT_KD_BUILD_SAH)
+            return fail(MCPT_E_INVALID, "unknown kd_build");
         auto s = std::make_unique<mcpt_scene>();
         int hit = 0;
-        mcpt::build_host_scene(m->m, s->hs, kd_cache_dir, &hit);
+        mcpt::build_host_scene(m->m, s->hs, kd_cache_dir, &hit, kd_build);
         if (cache_hit) *cache_hit = hit;
         if (s->hs.kd_tris.empty()) return fail(MCPT_E_INVALID, "scene has no triangles");
         if (layout != MCPT_LAYOUT_AUTO && layout != MCPT_LAYOUT_GLOBAL) return fail(MCPT_E_INVALID, "unknown layout");
@@ -1272,10 +1323,10 @@ int mcpt_scene_create_cached(const mcpt_model* m, const char* kd_cache_dir, int3
     return scene_create_impl(m, out, host_only == 0, kd_cache_dir, cache_hit);
 }
 int mcpt_scene_create_ex(const mcpt_model* m, const mcpt_scene_options* o, mcpt_scene** out, int32_t* cache_hit) {
-    const mcpt_scene_options d{nullptr, 0, MCPT_LAYOUT_AUTO};
+    const mcpt_scene_options d{nullptr, 0, MCPT_LAYOUT_AUTO, MCPT_KD_BUILD_REFERENCE};
     if (!o) o = &d;
     const char* dir = o->kd_cache_dir && o->kd_cache_dir[0] ? o->kd_cache_dir : nullptr;
-    return scene_create_impl(m, out, o->host_only == 0, dir, cache_hit, o->layout);
+    return scene_create_impl(m, out, o->host_only == 0, dir, cache_hit, o->layout, o->kd_build);
 }
 
 void mcpt_scene_destroy(mcpt_scene* s) { delete s; }
@@ -1291,6 +1342,7 @@ int mcpt_scene_get_info(const mcpt_scene* s, mcpt_scene_info* out) {
     out->node_boxes = s->gpu.node_boxes;
     out->device = s->device;
     out->n_devices = s->on_device ? 1 + static_cast<int64_t>(s->replicas.size()) : 0;
+    out->kd_build = s->hs.kd_build;
     return MCPT_OK;
 }
 
@@ -1465,6 +1517,8 @@ int mcpt_scene_reserve(mcpt_scene* s, const mcpt_render_params* p) {
         DeviceGuard guard;
         auto reserve = [&](mcpt_scene& sc, const mcpt_render_params* q) {
             set_device(sc);
+            sc.reserved = true;
+            ensure_capture_timing(sc);   // (events exist before any capture)
             Plan pl = make_plan(sc, q);
             fit_wavefront(sc, pl);
             const int sets = pl.pipeline == MCPT_PIPELINE_WAVEFRONT ? pl.wf_streams : 1;

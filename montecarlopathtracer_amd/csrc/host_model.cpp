@@ -386,7 +386,7 @@ void read_obj_cv(const std::string& path, ObjModel& m) {   // ObjReader.cpp:8-16
 }
 
 // ---------------------------------------------------------------------------
-void build_host_scene(const ObjModel& m, HostScene& hs, const char* kd_cache_dir, int* cache_hit) {
+void build_host_scene(const ObjModel& m, HostScene& hs, const char* kd_cache_dir, int* cache_hit, int kd_build) {
     hs = HostScene();
     const int64_t ntri = static_cast<int64_t>(m.triangles.size());
     // CreateGeometry (CUTracer.cu:277-311): one record per non-empty group,
@@ -445,16 +445,17 @@ void build_host_scene(const ObjModel& m, HostScene& hs, const char* kd_cache_dir
         }
     }
     if (cache_hit) *cache_hit = 0;
+    hs.kd_build = kd_build;
     if (kd_cache_dir && *kd_cache_dir) {
-        if (kd_cache_load(kd_cache_dir, hs.kd_verts, hs.nodes, hs.leaf_ids, hs.kd_depth)) {
+        if (kd_cache_load(kd_cache_dir, hs.kd_verts, hs.nodes, hs.leaf_ids, hs.kd_depth, kd_build)) {
             if (cache_hit) *cache_hit = 1;
             return;
         }
-        build_kdtree(hs.kd_verts, hs.nodes, hs.leaf_ids, hs.kd_depth);
-        kd_cache_store(kd_cache_dir, hs.kd_verts, hs.nodes, hs.leaf_ids, hs.kd_depth);   // best effort
+        build_kdtree(hs.kd_verts, hs.nodes, hs.leaf_ids, hs.kd_depth, kd_build);
+        kd_cache_store(kd_cache_dir, hs.kd_verts, hs.nodes, hs.leaf_ids, hs.kd_depth, kd_build);   // best effort
         return;
     }
-    build_kdtree(hs.kd_verts, hs.nodes, hs.leaf_ids, hs.kd_depth);
+    build_kdtree(hs.kd_verts, hs.nodes, hs.leaf_ids, hs.kd_depth, kd_build);
 }
 
 // ---------------------------------------------------------------------------
@@ -488,6 +489,7 @@ struct Box {
 
 struct BNode {
     Box box;
+    Box region;                  // kd_build SAH: the split-plane region (not clipped to the triangles)
     std::vector<uint32_t> ids;   // ascending (std::set<UINT>)
     uint32_t axis = 0;
     float split = 0.0f;
@@ -506,10 +508,80 @@ inline void classify(const Box& tb, int a, float v, FL&& to_left, FR&& to_right)
     }
 }
 
+// kd_build = MCPT_KD_BUILD_SAH (not the reference's rule): every node,
+// whatever its size, takes the split of least surface-area cost with a
+// traversal term -- cost = Ct + Ci (A_L n_L + A_R n_R) / A, against the
+// leaf's Ci n (Wald & Havran, "On building fast kd-trees for ray tracing, and
+// on doing that in O(N log N)", 2006; no empty-space bonus) -- where the areas
+// are those of the node's split-plane REGION cut at the plane (the space the
+// ordered walk's intervals cover; the reference's SAH uses the child boxes
+// clipped to the triangles and Ct = 0, KDTree.hpp:166) and the candidates are
+// the faces of the triangles' boxes strictly inside the region, so empty
+// space can be cut off.  One sweep per axis over sorted box ends: candidates
+// in ascending order per axis, axes 0..2, the first strict minimum wins (the
+// oracle, oracle/kdtree_ref.c, restates exactly this).  Triangle classification,
+// child boxes, depth cap and the BFS flatten are the reference's.  Priced on
+// the C1 frame: inner visits -43%, leaf visits -42%, triangle tests -5%.
+constexpr float kSahCt = 1.0f, kSahCi = 1.5f;
+struct SahScratch {
+    std::vector<float> mins, maxs, plan, cand;
+};
+bool sah_split(const std::vector<Box>& tbox, const std::vector<uint32_t>& ids, const Box& R, SahScratch& w,
+               int& ax, float& val) {
+    const float sz[3] = {R.mx[0] - R.mn[0], R.mx[1] - R.mn[1], R.mx[2] - R.mn[2]};
+    const float A0 = sz[0] * sz[1] + sz[1] * sz[2] + sz[2] * sz[0];
+    if (!(A0 > 0.0f)) return false;
+    const size_t n = ids.size();
+    float best = kSahCi * static_cast<float>(n);
+    bool found = false;
+    for (int a = 0; a < 3; ++a) {
+        w.mins.clear(); w.maxs.clear(); w.plan.clear(); w.cand.clear();
+        for (uint32_t id : ids) {
+            const float lo = tbox[id].mn[a], hi = tbox[id].mx[a];
+            w.mins.push_back(lo);
+            w.maxs.push_back(hi);
+            if (lo == hi) w.plan.push_back(lo);
+            // (+ 0.0f: a -0 candidate becomes +0, one value whatever the sort order of equal keys)
+            if (R.mn[a] < lo && lo < R.mx[a]) w.cand.push_back(lo + 0.0f);
+            if (R.mn[a] < hi && hi < R.mx[a]) w.cand.push_back(hi + 0.0f);
+        }
+        std::sort(w.mins.begin(), w.mins.end());
+        std::sort(w.maxs.begin(), w.maxs.end());
+        std::sort(w.plan.begin(), w.plan.end());
+        std::sort(w.cand.begin(), w.cand.end());
+        size_t im = 0, ix = 0, ip = 0;
+        for (size_t q = 0; q < w.cand.size(); ++q) {
+            if (q > 0 && !(w.cand[q - 1] < w.cand[q])) continue;
+            const float v = w.cand[q];
+            while (im < n && w.mins[im] < v) ++im;             // min < v: left
+            while (ix < n && !(v < w.maxs[ix])) ++ix;          // max <= v: not right
+            while (ip < w.plan.size() && w.plan[ip] < v) ++ip;
+            size_t jp = ip;
+            while (jp < w.plan.size() && !(v < w.plan[jp])) ++jp;   // flat on the plane: left
+            const float nL = static_cast<float>(im + (jp - ip)), nR = static_cast<float>(n - ix);
+            float sL[3] = {sz[0], sz[1], sz[2]}, sR[3] = {sz[0], sz[1], sz[2]};
+            sL[a] = v - R.mn[a];
+            sR[a] = R.mx[a] - v;
+            const float AL = sL[0] * sL[1] + sL[1] * sL[2] + sL[2] * sL[0];
+            const float AR = sR[0] * sR[1] + sR[1] * sR[2] + sR[2] * sR[0];
+            const float cost = kSahCt + kSahCi * ((AL * nL + AR * nR) / A0);
+            if (cost < best) {
+                best = cost;
+                ax = a;
+                val = v;
+                found = true;
+            }
+        }
+    }
+    return found;
+}
+
 }  // namespace
 
 void build_kdtree(const std::vector<float>& tv, std::vector<KdNode>& out,
-                  std::vector<uint32_t>& leaf_ids, int& depth_out) {
+                  std::vector<uint32_t>& leaf_ids, int& depth_out, int kd_build) {
+    if (kd_build != MCPT_KD_BUILD_REFERENCE && kd_build != MCPT_KD_BUILD_SAH)
+        throw Error{MCPT_E_INVALID, "unknown kd_build"};
     const size_t n = tv.size() / 9;
     std::vector<Box> tbox(n);
     for (size_t k = 0; k < n; ++k) {
@@ -528,7 +600,9 @@ void build_kdtree(const std::vector<float>& tv, std::vector<KdNode>& out,
     nodes[0].ids.resize(n);
     std::iota(nodes[0].ids.begin(), nodes[0].ids.end(), 0u);
     nodes[0].box = node_box(nodes[0].ids);
+    nodes[0].region = nodes[0].box;
     std::deque<int32_t> work{0};
+    SahScratch sah;
     int max_depth = 0;
     // The reference duplicates straddling triangles into both children down to
     // depth 32 (KDTree.hpp:103-153): triangles that straddle every split (long
@@ -554,7 +628,9 @@ void build_kdtree(const std::vector<float>& tv, std::vector<KdNode>& out,
         const std::vector<uint32_t>& ids = nodes[ni].ids;
         int ax = -1;
         float val = 0.0f;
-        if (ids.size() > 64u) {
+        if (kd_build == MCPT_KD_BUILD_SAH) {
+            if (!sah_split(tbox, ids, nodes[ni].region, sah, ax, val)) ax = -1;
+        } else if (ids.size() > 64u) {
             // spatial median of the longest axis (KDTree.hpp:108-122)
             float sz[3] = {box.mx[0] - box.mn[0], box.mx[1] - box.mn[1], box.mx[2] - box.mn[2]};
             ax = 0;
@@ -597,6 +673,8 @@ void build_kdtree(const std::vector<float>& tv, std::vector<KdNode>& out,
         BNode l, r;
         l.box = box; l.box.mx[ax] = val;
         r.box = box; r.box.mn[ax] = val;
+        l.region = nodes[ni].region; l.region.mx[ax] = val;
+        r.region = nodes[ni].region; r.region.mn[ax] = val;
         for (uint32_t id : ids)
             classify(tbox[id], ax, val, [&] { l.ids.push_back(id); }, [&] { r.ids.push_back(id); });
         l.box.clip(node_box(l.ids));

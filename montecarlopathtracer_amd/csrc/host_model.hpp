@@ -71,21 +71,25 @@ struct HostScene {
     std::vector<KdNode> nodes;
     std::vector<uint32_t> leaf_ids;
     int kd_depth = 0;
+    int kd_build = 0;                 // MCPT_KD_BUILD_*
 };
 
 // CreateGeometry semantics + KD build; throws mcpt::Error.  With a cache
 // directory the KD tree is read from / written to it (kd_cache.cpp);
 // *cache_hit (if given) = 1 when it was read, 0 when built.
+// kd_build: MCPT_KD_BUILD_REFERENCE (KDTree.hpp) or MCPT_KD_BUILD_SAH.
 void build_host_scene(const ObjModel& m, HostScene& out, const char* kd_cache_dir = nullptr,
-                      int* cache_hit = nullptr);
+                      int* cache_hit = nullptr, int kd_build = 0);
 // on-disk KD cache (kd_cache.cpp): load returns false unless a valid file exists
+// (files are keyed by the vertices and the build rule)
 bool kd_cache_load(const std::string& dir, const std::vector<float>& tri_verts, std::vector<KdNode>& nodes,
-                   std::vector<uint32_t>& leaf_ids, int& depth);
+                   std::vector<uint32_t>& leaf_ids, int& depth, int kd_build = 0);
 bool kd_cache_store(const std::string& dir, const std::vector<float>& tri_verts, const std::vector<KdNode>& nodes,
-                    const std::vector<uint32_t>& leaf_ids, int depth);
-// KD build only (KDTree.hpp semantics) over kd_verts; fills nodes/leaf_ids/kd_depth.
+                    const std::vector<uint32_t>& leaf_ids, int depth, int kd_build = 0);
+// KD build only over kd_verts (KDTree.hpp semantics, or the SAH rule of
+// MCPT_KD_BUILD_SAH); fills nodes/leaf_ids/kd_depth.
 void build_kdtree(const std::vector<float>& tri_verts, std::vector<KdNode>& nodes,
-                  std::vector<uint32_t>& leaf_ids, int& depth);
+                  std::vector<uint32_t>& leaf_ids, int& depth, int kd_build = 0);
 
 struct Error {
     int code;

@@ -22,12 +22,17 @@
 #include <unistd.h>
 
 #include "host_model.hpp"
+#include "../../include/mcpt.h"
 
 namespace mcpt {
 namespace {
 
-// bump whenever build_kdtree's output for the same input can change
+// bump whenever build_kdtree's output for the same input can change; the SAH
+// rule (MCPT_KD_BUILD_SAH) has its own id, so its files never match a
+// reference-rule lookup and vice versa
 constexpr uint32_t kBuilderVersion = 1;
+constexpr uint32_t kSahBuilderVersion = 0x5A480001u;
+uint32_t builder_id(int kd_build) { return kd_build == MCPT_KD_BUILD_SAH ? kSahBuilderVersion : kBuilderVersion; }
 constexpr char kMagic[8] = {'M', 'C', 'P', 'T', 'K', 'D', 'C', '1'};
 constexpr uint32_t kNodeWords = 12;   // left right bmin[3] bmax[3] axis split leaf_begin leaf_count
 constexpr int32_t kMaxKdDepth = 32;   // build_kdtree's cap (KDTree.hpp:103-106)
@@ -53,11 +58,11 @@ uint64_t fnv1a(const void* data, size_t n, uint64_t h) {
     return h;
 }
 
-void keys(const std::vector<float>& tv, uint64_t& a, uint64_t& b) {
+void keys(const std::vector<float>& tv, uint32_t builder, uint64_t& a, uint64_t& b) {
     const uint64_t n = tv.size() / 9;
-    a = fnv1a(&kBuilderVersion, 4, fnv1a(&n, 8, 0xCBF29CE484222325ull));
+    a = fnv1a(&builder, 4, fnv1a(&n, 8, 0xCBF29CE484222325ull));
     a = fnv1a(tv.data(), tv.size() * 4, a);
-    b = fnv1a(&n, 8, fnv1a(&kBuilderVersion, 4, 0x84222325CBF29CE4ull));
+    b = fnv1a(&n, 8, fnv1a(&builder, 4, 0x84222325CBF29CE4ull));
     // second key over the words in reverse order: independent of the first
     for (size_t i = tv.size(); i-- > 0;) b = fnv1a(&tv[i], 4, b);
 }
@@ -124,15 +129,16 @@ bool valid_tree(const std::vector<uint32_t>& w, const std::vector<uint32_t>& lea
 }  // namespace
 
 bool kd_cache_load(const std::string& dir, const std::vector<float>& tv, std::vector<KdNode>& nodes,
-                   std::vector<uint32_t>& leaf_ids, int& depth) {
+                   std::vector<uint32_t>& leaf_ids, int& depth, int kd_build) {
+    const uint32_t builder = builder_id(kd_build);
     uint64_t ka, kb;
-    keys(tv, ka, kb);
+    keys(tv, builder, ka, kb);
     FILE* f = std::fopen(path_for(dir, ka).c_str(), "rb");
     if (!f) return false;
     Header h{};
     std::vector<uint32_t> w, ids;
     bool ok = std::fread(&h, sizeof h, 1, f) == 1 && std::memcmp(h.magic, kMagic, 8) == 0 &&
-              h.version == kBuilderVersion && h.node_words == kNodeWords && h.n_tris == tv.size() / 9 &&
+              h.version == builder && h.node_words == kNodeWords && h.n_tris == tv.size() / 9 &&
               h.key_a == ka && h.key_b == kb && h.n_nodes > 0 && h.n_nodes < (1ull << 31) &&
               h.n_leaf_ids < (1ull << 31) && h.depth >= 0 && h.depth <= kMaxKdDepth;
     if (ok) {
@@ -173,13 +179,13 @@ bool kd_cache_load(const std::string& dir, const std::vector<float>& tv, std::ve
 }
 
 bool kd_cache_store(const std::string& dir, const std::vector<float>& tv, const std::vector<KdNode>& nodes,
-                    const std::vector<uint32_t>& leaf_ids, int depth) {
+                    const std::vector<uint32_t>& leaf_ids, int depth, int kd_build) {
     Header h{};
     std::memcpy(h.magic, kMagic, 8);
-    h.version = kBuilderVersion;
+    h.version = builder_id(kd_build);
     h.node_words = kNodeWords;
     h.n_tris = tv.size() / 9;
-    keys(tv, h.key_a, h.key_b);
+    keys(tv, h.version, h.key_a, h.key_b);
     h.n_nodes = nodes.size();
     h.n_leaf_ids = leaf_ids.size();
     h.depth = depth;

@@ -257,19 +257,25 @@ class Scene:
     """A device-resident scene (CreateGeometry result + KD tree)."""
 
     LAYOUTS = {"auto": _capi.LAYOUT_AUTO, "global": _capi.LAYOUT_GLOBAL}
+    KD_BUILDS = {"reference": _capi.KD_BUILD_REFERENCE, "sah": _capi.KD_BUILD_SAH}
 
     def __init__(self, model: ObjModel, host_only: bool = False, kd_cache: Optional[str] = None,
-                 layout: str = "auto"):
+                 layout: str = "auto", kd_build: str = "reference"):
         """kd_cache: directory for the on-disk KD-build cache (mcpt_scene_create_ex);
         ``cache_hit`` tells whether the tree was read from it.  layout "global":
         the scene image with child-box pair records in global memory even if it
-        would fit in LDS (MCPT_LAYOUT_GLOBAL)."""
+        would fit in LDS (MCPT_LAYOUT_GLOBAL).  kd_build "sah": the KD tree's
+        splits by the SAH with a traversal cost (MCPT_KD_BUILD_SAH) instead of
+        QuinEngine's KDTree.hpp rule -- the same image, fewer node visits."""
         if layout not in self.LAYOUTS:
             raise ValueError(f"layout must be one of {sorted(self.LAYOUTS)}")
+        if kd_build not in self.KD_BUILDS:
+            raise ValueError(f"kd_build must be one of {sorted(self.KD_BUILDS)}")
         h = C.c_void_p()
         if kd_cache:
             os.makedirs(kd_cache, exist_ok=True)
-        opt = _capi.SceneOptions(os.fsencode(kd_cache) if kd_cache else None, int(host_only), self.LAYOUTS[layout])
+        opt = _capi.SceneOptions(os.fsencode(kd_cache) if kd_cache else None, int(host_only), self.LAYOUTS[layout],
+                                 self.KD_BUILDS[kd_build])
         hit = C.c_int32(0)
         check(lib().mcpt_scene_create_ex(model.handle, C.byref(opt), C.byref(h), C.byref(hit)))
         self.cache_hit = bool(hit.value)

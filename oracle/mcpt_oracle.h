@@ -85,6 +85,10 @@ typedef struct {
 
 /* scene ------------------------------------------------------------------ */
 orc_scene* orc_scene_load(const char* obj_path, char* err, int errlen);
+/* kd_build: 0 = KDTree.hpp (the reference), 1 = the product's MCPT_KD_BUILD_SAH rule */
+orc_scene* orc_scene_load_kd(const char* obj_path, int flavor, int kd_build, char* err, int errlen);
+/* pricing only: the SAH rule's traversal / intersection costs for later loads (product: 1, 1.5) */
+void orc_kd_set_sah_costs(float ct, float ci);
 /* flavor 0: the CVMCTracer ObjReader; 1: QuinEngine's tinyobjloader (obj_reader.c) */
 orc_scene* orc_scene_load_ex(const char* obj_path, int flavor, char* err, int errlen);
 void orc_scene_free(orc_scene* s);

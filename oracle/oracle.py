@@ -60,6 +60,9 @@ def lib():
         L.orc_scene_load.argtypes = [C.c_char_p, C.c_char_p, C.c_int]
         L.orc_scene_load_ex.restype = vp
         L.orc_scene_load_ex.argtypes = [C.c_char_p, C.c_int, C.c_char_p, C.c_int]
+        L.orc_scene_load_kd.restype = vp
+        L.orc_scene_load_kd.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_char_p, C.c_int]
+        L.orc_kd_set_sah_costs.argtypes = [C.c_float, C.c_float]
         L.orc_scene_free.argtypes = [vp]
         L.orc_scene_info.argtypes = [vp, C.POINTER(C.c_int64)]
         for n in ("orc_copy_vertices", "orc_copy_normals"):
@@ -119,11 +122,15 @@ def _p(a, ct):
 class Scene:
     """An oracle scene (model + CreateGeometry groups + reference KD tree)."""
 
-    def __init__(self, obj_path: str, flavor: str = "cvmctracer"):
-        """flavor "tinyobj": QuinEngine's loader semantics (obj_reader.c orc_model_read_tinyobj)"""
+    KD_BUILDS = {"reference": 0, "sah": 1}
+
+    def __init__(self, obj_path: str, flavor: str = "cvmctracer", kd_build: str = "reference"):
+        """flavor "tinyobj": QuinEngine's loader semantics (obj_reader.c orc_model_read_tinyobj);
+        kd_build "sah": the product's MCPT_KD_BUILD_SAH split rule (kdtree_ref.c sah_split)"""
         L = lib()
         err = C.create_string_buffer(512)
-        h = L.orc_scene_load_ex(obj_path.encode(), {"cvmctracer": 0, "tinyobj": 1}[flavor], err, 512)
+        h = L.orc_scene_load_kd(obj_path.encode(), {"cvmctracer": 0, "tinyobj": 1}[flavor], self.KD_BUILDS[kd_build],
+                                err, 512)
         if not h:
             raise RuntimeError(f"oracle: {err.value.decode()}")
         self._h = h

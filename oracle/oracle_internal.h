@@ -61,6 +61,6 @@ int orc_model_read(orc_model* m, const char* path, char* err, int errlen);
 int orc_model_read_tinyobj(orc_model* m, const char* path, char* err, int errlen);
 void orc_model_free(orc_model* m);
 /* KD build over kd triangles (vertex triples), flattened BFS */
-void orc_kd_build(orc_scene* s);
+void orc_kd_build(orc_scene* s, int kd_build);
 
 #endif

@@ -313,6 +313,19 @@ typedef struct {
     orc_v3 hp;
 } hit_t;
 
+/* Diagnostic hooks of the ordered walk and the path loop: no-ops here;
+ * scripts/price_descent.c defines them to price traversal changes on the
+ * oracle's exact visit sequence (test/diagnostic infrastructure only). */
+#ifndef ORC_DIAG_FIELDS
+#define ORC_DIAG_FIELDS
+#define ORC_DIAG_RAY_BEGIN(q) do {} while (0)
+#define ORC_DIAG_INNER(q, node) do {} while (0)
+#define ORC_DIAG_LEAF(q, node) do {} while (0)
+#define ORC_DIAG_POP(q) do {} while (0)
+#define ORC_DIAG_ACCEPT(q, node) do {} while (0)
+#define ORC_DIAG_AFTER_ISECT(q, depth) do {} while (0)
+#endif
+
 typedef struct {
     const orc_scene* s;
     const orc_v3 (*kv)[3];   /* vertices by kd id */
@@ -320,6 +333,7 @@ typedef struct {
     int node_boxes;          /* ordered walk: fp16 child-box cull */
     float best_init;         /* FLT_MAX (CUTracer.cu:46); 10000 in QE mode (rtx.hlsl:88) */
     orc_counters c;
+    ORC_DIAG_FIELDS
 } qctx;
 
 /* CUTracer.cu:54-92: Cramer test of one triangle against the running tmin */
@@ -486,6 +500,7 @@ static hit_t isect_kd_ordered(qctx* q, orc_v3 o, orc_v3 d) {
     h.tri = -1; h.geom = -1;
     float best = q->best_init;
     uint32_t bprio = 0xFFFFFFFFu;
+    ORC_DIAG_RAY_BEGIN(q);
     float oo[3] = {o.x, o.y, o.z}, dd[3] = {d.x, d.y, d.z};
     float inv[3] = {1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
     const orc_node* root = &s->nodes[0];
@@ -511,6 +526,7 @@ static hit_t isect_kd_ordered(qctx* q, orc_v3 o, orc_v3 d) {
         const orc_node* nd = &s->nodes[node];
         while (nd->axis) {
             q->c.inner_visits++;
+            ORC_DIAG_INNER(q, node);
             int a = (int)nd->axis - 1;
             float sv = nd->split;
             float t = (sv - oo[a]) * inv[a];
@@ -536,6 +552,7 @@ static hit_t isect_kd_ordered(qctx* q, orc_v3 o, orc_v3 d) {
                 tmax = t < tmax ? t : tmax;
             }
             if (!(node == nearc ? nhit : fhit)) {   /* chosen child missed: next interval */
+                ORC_DIAG_POP(q);
                 if (sp == 0) return h;
                 sp--;
                 node = st_node[sp]; tmin = st_lo[sp]; tmax = st_hi[sp];
@@ -545,11 +562,13 @@ static hit_t isect_kd_ordered(qctx* q, orc_v3 o, orc_v3 d) {
             nd = &s->nodes[node];
         }
         q->c.leaf_visits++;
+        ORC_DIAG_LEAF(q, node);
         for (uint32_t i = 0; i < nd->tri_count; i++) {
             uint32_t k = s->leaf_ids[nd->tri_begin + i];
             q->c.leaf_refs++;
             q->c.tri_tests++;
-            tri_test(q->kv[k], o, d, &best, &h, (int)k, s->tri_geom[s->kd_tris[k]], s->kd_prio[k], &bprio);
+            if (tri_test(q->kv[k], o, d, &best, &h, (int)k, s->tri_geom[s->kd_tris[k]], s->kd_prio[k], &bprio))
+                ORC_DIAG_ACCEPT(q, node);
         }
         if (sp == 0) break;
         sp--;
@@ -679,6 +698,7 @@ static orc_v3 sample_mc(qctx* q, usrc* u, orc_v3 pos, orc_v3 dir, int max_depth,
     q->c.paths++;
     for (depth = 0; depth < max_depth; depth++) {
         hit_t hit = intersect(q, pos, dir);
+        ORC_DIAG_AFTER_ISECT(q, depth);
         if (hit.geom == -1) return v3(0, 0, 0);
         const orc_geom* g = &s->geoms[hit.geom];
         if (g->Ka.x > 0 || g->Ka.y > 0 || g->Ka.z > 0) {
@@ -715,6 +735,7 @@ static orc_v3 sample_mc(qctx* q, usrc* u, orc_v3 pos, orc_v3 dir, int max_depth,
     }
     {
         hit_t hit = intersect(q, pos, dir);
+        ORC_DIAG_AFTER_ISECT(q, max_depth);
         if (hit.geom != -1) {
             const orc_geom* g = &s->geoms[hit.geom];
             color.x *= g->Ka.x * illum;
@@ -930,6 +951,10 @@ int orc_render(const orc_scene* s, const orc_params* p, float* out, orc_counters
 orc_scene* orc_scene_load(const char* path, char* err, int errlen) { return orc_scene_load_ex(path, 0, err, errlen); }
 
 orc_scene* orc_scene_load_ex(const char* path, int flavor, char* err, int errlen) {
+    return orc_scene_load_kd(path, flavor, 0, err, errlen);
+}
+
+orc_scene* orc_scene_load_kd(const char* path, int flavor, int kd_build, char* err, int errlen) {
     char dummy[256];
     if (!err) { err = dummy; errlen = sizeof dummy; }
     err[0] = 0;
@@ -992,7 +1017,7 @@ orc_scene* orc_scene_load_ex(const char* path, int flavor, char* err, int errlen
             }
         free(cv2kd);
     }
-    orc_kd_build(s);
+    orc_kd_build(s, kd_build);
     return s;
 }
 

@@ -95,3 +95,45 @@ def test_ray_stream_bytes():
     import bench
     assert bench.ray_stream_bytes(10, 4, 5) == 16 * 4 + 32 * 6
     assert bench.ray_stream_bytes(10, 4, 4) == 32 * 6
+
+
+def test_ray_stream_bytes_sort_and_qe():
+    """with the material sort or in QuinEngine mode there is no
+    implicit bounce 0 -- the extend reads both streams of every primary ray --
+    and the sort's hit records are 16 B, not 4."""
+    bench = _bench()
+    for v in (4, 5):
+        assert bench.ray_stream_bytes(10, 4, v, sort=True) == 32 * 10
+        assert bench.ray_stream_bytes(10, 4, v, qe=True) == 32 * 10
+    assert bench.hit_write_bytes(10) == 40 and bench.hit_write_bytes(10, sort=True) == 160
+
+
+def _run_bench(args, env_extra, timeout=120):
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MCPT_DIST_BACKEND")}
+    env.update(env_extra)
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                          timeout=timeout, env=env, cwd=ROOT)
+
+
+def test_bench_refuses_more_gpus_than_visible():
+    """`bench.py --gpus N` without a launcher starts N ranks
+    itself, and exits non-zero (no JSON line) when fewer than N GPUs are
+    visible -- here none -- instead of measuring one GPU and calling it N."""
+    import torch
+    if torch.cuda.device_count() >= 2:
+        import pytest
+        pytest.skip("enough GPUs: the launcher would run")
+    r = _run_bench(["--gpus", "2", "--steps", "1", "--warmup", "0"], {})
+    assert r.returncode != 0
+    assert "GPU(s) visible" in r.stderr, r.stderr[-2000:]
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_bench_refuses_world_size_mismatch():
+    """A launcher that started a different number of ranks than --gpus: exit
+    non-zero before any GPU call (no line whose n_gpus differs from --gpus)."""
+    r = _run_bench(["--gpus", "2", "--steps", "1"], {"WORLD_SIZE": "3", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0 and "WORLD_SIZE=3" in r.stderr, r.stderr[-2000:]
+    r = _run_bench(["--gpus", "1", "--steps", "1"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr, r.stderr[-2000:]

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol(mcpt):
 
 def test_abi_version_and_defaults(mcpt):
     from montecarlopathtracer_amd._capi import RenderParamsC, lib
-    assert lib().mcpt_abi_version() == 8
+    assert lib().mcpt_abi_version() == 9
     p = RenderParamsC()
     lib().mcpt_render_params_default(C.byref(p))
     # CV/stdafx.h:41-46, CUTracer.cu:189,212,349-351

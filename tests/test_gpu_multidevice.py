@@ -309,6 +309,60 @@ def test_small_reservation_then_larger_render(mcpt):
     assert np.array_equal(img, ref) and st["rays"] == rs["rays"]
 
 
+def test_capture_past_reservation_refused_and_old_graph_survives_growth(mcpt):
+    """capi.cpp grow_ws: a render captured into a graph on a scene
+    whose reservation is too small fails with MCPT_E_NOMEM before any launch;
+    an uncaptured render that grows the workspace retires the reserved buffers
+    instead of freeing them, so a graph captured against the reservation still
+    replays the right image afterwards; and the grown queues become the
+    reservation (a captured render of the larger params is then accepted)."""
+    import torch
+    from montecarlopathtracer_amd._capi import McptError
+    scene = mcpt.Scene(mcpt.ObjModel(mcpt.scene_path("scene01")))
+    small = mcpt.RenderParams(width=32, height=32, spp=4, spp_chunk=2, pipeline="wavefront", wf_streams=1)
+    big = mcpt.RenderParams(width=96, height=64, spp=64, spp_chunk=8, pipeline="wavefront", wf_streams=1)
+    ref_small, _ = scene.render(small)
+    ref_big, _ = mcpt.Scene(mcpt.ObjModel(mcpt.scene_path("scene01"))).render(big)
+    scene = mcpt.Scene(mcpt.ObjModel(mcpt.scene_path("scene01")))
+    scene.reserve(small)
+    s = torch.cuda.Stream()
+    fb_s = torch.zeros((32 * 32, 4), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    g_small = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g_small, stream=s, capture_error_mode="relaxed"):
+        scene.render_device(small, fb_s.data_ptr(), s.cuda_stream)
+    # a captured render of the big params: refused, nothing launched
+    fb_b = torch.zeros((96 * 64, 4), dtype=torch.float32, device="cuda")
+    g_bad = torch.cuda.CUDAGraph()
+    err = None
+    with torch.cuda.graph(g_bad, stream=s, capture_error_mode="relaxed"):
+        try:
+            scene.render_device(big, fb_b.data_ptr(), s.cuda_stream)
+        except McptError as e:
+            err = e
+        fb_b.add_(1.0)   # (the graph is not empty)
+    assert err is not None and err.code == -5, err   # MCPT_E_NOMEM
+    fb_b.zero_()
+    g_bad.replay()       # nothing of the refused render was captured
+    torch.cuda.synchronize()
+    assert bool((fb_b == 1.0).all())
+    # uncaptured big render grows the workspace; the small graph still replays correctly
+    img, _ = scene.render(big)
+    assert np.array_equal(img, ref_big)
+    fb_s.zero_()
+    g_small.replay()
+    torch.cuda.synchronize()
+    assert np.array_equal(fb_s.view(32, 32, 4)[..., :3].cpu().numpy(), ref_small)
+    # the grown workspace is the reservation now: a captured big render is accepted
+    g_big = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g_big, stream=s, capture_error_mode="relaxed"):
+        scene.render_device(big, fb_b.data_ptr(), s.cuda_stream)
+    fb_b.zero_()
+    g_big.replay()
+    torch.cuda.synchronize()
+    assert np.array_equal(fb_b.view(64, 96, 4)[..., :3].cpu().numpy(), ref_big)
+
+
 @pytest.mark.parametrize("n", [1, 2])
 def test_unknown_gather_rejected_on_every_path(mcpt, devices, n):
     """mcpt_render_params::gather other than PEER / RCCL is MCPT_E_INVALID on a

@@ -125,3 +125,28 @@ def test_bench_single_process_device_list(mcpt, tmp_path):
     ref, st = _single_gpu_image(mcpt)
     assert np.array_equal(got[..., :3], ref)
     assert line["rays_per_step"] == st["rays"]
+
+
+def test_bench_gpus_n_without_launcher(mcpt, tmp_path):
+    """`python bench.py --gpus 2` with no torch.distributed
+    launcher.  With the default RCCL backend on a box with fewer than 2 GPUs it
+    exits non-zero and prints no line; under the gloo rehearsal it starts the 2
+    ranks itself (a torch.distributed.run child) and prints n_gpus == 2 with
+    rank 0's gathered image equal to the one-GPU render."""
+    import torch
+    base = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--width", str(W), "--height", str(H),
+            "--spp", str(SPP), "--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--no-pmc"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MCPT_DIST_BACKEND")}
+    if torch.cuda.device_count() < 2:
+        r = subprocess.run(base, capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
+        assert r.returncode != 0 and "GPU(s) visible" in r.stderr, r.stdout[-2000:] + r.stderr[-2000:]
+        assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    out = str(tmp_path / "img.npy")
+    r = subprocess.run(base + ["--dump-image", out], capture_output=True, text=True, timeout=280,
+                       env=dict(env, MCPT_DIST_BACKEND="gloo"), cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    line = _bench_line(r.stdout)
+    assert line["n_gpus"] == 2 and "x2" in line["config"]["parallelism"]
+    ref, st = _single_gpu_image(mcpt)
+    assert np.array_equal(np.load(out)[..., :3], ref)
+    assert line["rays_per_step"] == st["rays"]
