@@ -92,3 +92,74 @@ def test_shipped_kernels_fit_16_waves_per_cu(tmp_path):
     for name, r in kernels.items():
         if "wf_" in name:
             assert r["scratch"] == 0, (name, r)
+
+
+def _disasm(lib, tmp_path):
+    """kernel name -> its instruction lines (mnemonic first), from the shipped code objects"""
+    out = {}
+    for co in _code_objects(lib, tmp_path):
+        txt = subprocess.run([os.path.join(LLVM, "llvm-objdump"), "-d", "--no-show-raw-insn", str(co)], check=True,
+                             capture_output=True, text=True).stdout
+        cur = None
+        for line in txt.splitlines():
+            m = re.match(r"^[0-9a-f]+ <(\S+)>:$", line.strip())
+            if m:
+                cur = m.group(1)
+                out[cur] = []
+            elif cur and line.strip() and not line.strip().startswith(";"):
+                out[cur].append(line.strip())
+    return out
+
+
+def test_codegen_flags_still_do_their_job(tmp_path):
+    """each per-source LLVM option in _build.py was adopted
+    for a measured gain; this pins, in the shipped code objects, the code
+    property each one produces, so a toolchain change that silently drops it
+    fails here.  Counts with / without the option (ROCm 7.2, measured by
+    compiling the source with the option removed):
+    * -amdgpu-set-wave-priority=1 (wavefront sources): an `s_setprio 3` around
+      the first vector-memory loads of every extend kernel (the source itself
+      only uses priorities 0 and 1): 1 / 0;
+    * -unroll-threshold=2000 (wavefront.hip, render.hip): the global-memory
+      variants' capped descent unrolled -- 12 fp16 box-bound conversions per
+      step (two child boxes), so 12 x cap of them: 60 / 12;
+    * -two-entry-phi-node-folding-threshold=8 (wavefront.hip): if-diamonds of
+      the global extend folded into selects -- exec-mask regions
+      (`s_and_saveexec_b64`) in the lean queue-order global extend: 83 / 103;
+    * -enable-gvn-hoist (render.hip): float products common to both sides of
+      a branch hoisted -- `v_mul_f32_e32` in the lean LDS / global megakernels:
+      181 / 184 and 277 / 281;
+    * -structurizecfg-skip-uniform-regions=1 (wavefront_primary.hip): uniform
+      branches of the bounce-0 packet walk kept as scalar branches instead of
+      exec-mask regions -- `s_cbranch_vccz` in its lean kernel: 5 / 14."""
+    if not os.path.exists(os.path.join(LLVM, "llvm-objdump")):
+        pytest.skip("ROCm llvm tools not available")
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("_b", os.path.join(ROOT, "montecarlopathtracer_amd", "_build.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    lib = b.build()
+    k = _disasm(lib, tmp_path)
+
+    def one(pat):
+        m = [n for n in k if re.search(pat, n)]
+        assert len(m) == 1, (pat, m)
+        return k[m[0]]
+
+    def count(ins, prefix):
+        return sum(1 for x in ins if x.split()[0].startswith(prefix))
+
+    extends = [n for n in k if "wf_extend" in n]
+    assert extends
+    for n in extends:
+        assert any(x.startswith("s_setprio 3") for x in k[n]), n
+    g_ext = one(r"wf_extendILi0ELi\d+ELi256ELb0ELb0E")       # global layout, lean, queue order
+    mk_glob = one(r"path_kernelILb0ELi8ELi256ELb0ELb1ELb0E")   # global layout, lean megakernel
+    mk_lds = one(r"path_kernelILb1ELi4ELi1024ELb0ELb0ELb0E")   # LDS layout, lean megakernel
+    cap = 5                                                     # MCPT_DESCENT_CAP_GLOBAL
+    assert count(g_ext, "v_cvt_f32_f16") >= 12 * cap
+    assert count(mk_glob, "v_cvt_f32_f16") >= 12 * cap
+    assert count(g_ext, "s_and_saveexec_b64") <= 93
+    assert count(mk_lds, "v_mul_f32_e32") <= 182 and count(mk_glob, "v_mul_f32_e32") <= 279
+    prim = one(r"wf_extend_primaryILi4ELi1024ELb0E")
+    assert count(prim, "s_cbranch_vccz") <= 9
