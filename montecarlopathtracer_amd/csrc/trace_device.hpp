@@ -262,6 +262,14 @@ __device__ __forceinline__ float4 ld_tri(const float4* __restrict__ p) {
 // address is known before the split-plane decision, so the LDS latency overlaps
 // the decision; stack entries carry the far child's record (16 B: w0, w1, lo,
 // hi), so a pop needs no node re-read.
+// Diagnostic builds only (-DMCPT_PHASE_MARKERS, scripts/phase_isa.py): a
+// marker pair `s_nop 15; s_nop n` at each phase boundary of the walk, so the
+// static instruction count of each phase can be read from the code object.
+#ifdef MCPT_PHASE_MARKERS
+#define MCPT_MARK(n) asm volatile("s_nop 15\n\ts_nop " #n ::: "memory")
+#else
+#define MCPT_MARK(n) do {} while (0)
+#endif
 #ifdef MCPT_PHASE_TIMING
 #define MCPT_LU_PARAM , LaneUse& lu
 #define MCPT_LU_ARG , lu
@@ -387,6 +395,7 @@ __device__ __forceinline__ int descend_steps(RayState& r, const uint2* __restric
     while ((w0 >> 30) != 3u) {
         if (steps == cap) return 0;           // resume next call
         steps++;
+        MCPT_MARK(1);
         if constexpr (COUNT) c.inner++;
         MCPT_LANE_USE(desc_w, desc_l, lu);
         const uint32_t left = w0 & kLeftMask;
@@ -462,6 +471,7 @@ __device__ __forceinline__ int descend_steps(RayState& r, const uint2* __restric
             }
         }
     }
+    MCPT_MARK(2);
     if constexpr (COUNT) c.leaf++;
     r.lpos = w0 & 0x3FFFFFFFu;
     r.lend = r.lpos + w1;
@@ -488,6 +498,7 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
     // the stack's top slot, read ahead: the pop after this leaf's last tests
     // then needs no LDS round trip of its own (unused if the leaf goes on or
     // the stack is empty -- the slot index is in range either way)
+    MCPT_MARK(3);
     const uint4 top = ld4(slot_of<S>(st, stride, r.sp - U));
     if (r.lpos < r.lend) {
         // both triangles' records are read before either test runs, so the two
@@ -509,6 +520,7 @@ __device__ __forceinline__ bool trav_iter(RayState& r, const float4* __restrict_
         test_tri_pair<!TRIS_LDS>(r, a0, a1, a2, k0, b0, b1, b2, k1, two);
         r.lpos += two ? 2u : 1u;
     }
+    MCPT_MARK(4);
     if (r.lpos < r.lend) return false;        // more triangles in this leaf
     return !pop_entry<S, !BOXES>(r, st, stride, spill, spill_stride, &top);
 }

@@ -431,7 +431,8 @@ wf_extend(const KernelParams kp, const WfParams wf) {
     };
 #ifdef MCPT_PHASE_TIMING
     // stats[8] setup, [9] traversal bursts, [10] hand-offs, [11] burst iterations
-    unsigned long long tm_setup = 0, tm_trav = 0, tm_hand = 0, tm_iters = 0, tm_t0 = __builtin_amdgcn_s_memtime();
+    unsigned long long tm_setup = 0, tm_trav = 0, tm_hand = 0, tm_iters = 0, tm_hands = 0,
+                       tm_t0 = __builtin_amdgcn_s_memtime();
 #define WF_STAMP(acc) do { unsigned long long t1_ = __builtin_amdgcn_s_memtime(); acc += t1_ - tm_t0; tm_t0 = t1_; } while (0)
 #else
 #define WF_STAMP(acc) do {} while (0)
@@ -459,17 +460,23 @@ wf_extend(const KernelParams kp, const WfParams wf) {
                 if ((threadIdx.x & 63u) == 0) { lu.burst_w += 1; lu.burst_l += (unsigned long long)__popcll(tv); }
             }
 #endif
+            MCPT_MARK(5);
             if (mode == kTrav) {
                 if (trav_iter<S, !IN_LDS, COUNT, LAY == kLayLds, IN_LDS ? kWfLdsCap : MCPT_WF_DESCENT_CAP_GLOBAL>(r, tris, nodes, leafs, st, BLOCK, spill, spill_stride, c MCPT_LU_ARG,
                                                  pairs))
                     mode = kReady;
             }
+            MCPT_MARK(6);
             const uint64_t trv = __ballot(mode == kTrav);
             const uint64_t rdy = __ballot(mode == kReady);
             if (!trv || (int)__popcll(rdy) >= refill) break;
         }
         WF_STAMP(tm_trav);
+#ifdef MCPT_PHASE_TIMING
+        tm_hands++;
+#endif
         // ---- hand-off: hit record + per-material class list -----------------
+        MCPT_MARK(7);
         __builtin_amdgcn_s_setprio(MCPT_WF_EXT_PRIO + 1);   // as the megakernel's shading rounds: short phase, raised priority
         // Settle the prefetch (issued a whole burst ago) before any store of
         // this hand-off: gfx9's vmcnt also counts stores, so any later wait on
@@ -531,6 +538,7 @@ wf_extend(const KernelParams kp, const WfParams wf) {
             }
         }
         WF_STAMP(tm_hand);
+        MCPT_MARK(8);
         if (!__ballot(mode != kDead)) break;
     }
     if constexpr (SORT) {
@@ -543,6 +551,7 @@ wf_extend(const KernelParams kp, const WfParams wf) {
         atomicAdd(kp.stats + 9, tm_trav);
         atomicAdd(kp.stats + 10, tm_hand);
         atomicAdd(kp.stats + 11, tm_iters);
+        atomicAdd(kp.stats + 12, tm_hands);
     }
     {
         unsigned long long* gl = reinterpret_cast<unsigned long long*>(&g_lane_use);
