@@ -522,7 +522,11 @@ inline void classify(const Box& tb, int a, float v, FL&& to_left, FR&& to_right)
 // oracle, oracle/kdtree_ref.c, restates exactly this).  Triangle classification,
 // child boxes, depth cap and the BFS flatten are the reference's.  Priced on
 // the C1 frame: inner visits -43%, leaf visits -42%, triangle tests -5%.
-constexpr float kSahCt = 1.0f, kSahCi = 1.5f;
+#ifndef MCPT_SAH_CT          // (A/B builds only; the oracle restates 1 and 1.5)
+#define MCPT_SAH_CT 1.0f
+#define MCPT_SAH_CI 1.5f
+#endif
+constexpr float kSahCt = MCPT_SAH_CT, kSahCi = MCPT_SAH_CI;
 struct SahScratch {
     std::vector<float> mins, maxs, plan, cand;
 };

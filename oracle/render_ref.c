@@ -477,20 +477,18 @@ uint16_t orc_f16_dir(float x, int dir) {
 /* does the ray segment (0, best] meet the node's fp16 box?  (trace_device.hpp box_hit) */
 static int box_hit(const orc_node* nd, const float* oo, const float* dd, const float* inv, float best) {
     float lo = 0.0f, hi = best;
-    int out = 0;
+    /* slab ends ordered by the direction's sign; inv = +-inf for a zero
+     * component makes each bound's term -inf / +inf inside / outside and NaN
+     * on it, which the comparisons pass over (the containment test) */
     for (int a = 0; a < 3; a++) {
         float blo = orc_f16_to_f32(orc_f16_dir(nd->bmin[a], -1));
         float bhi = orc_f16_to_f32(orc_f16_dir(nd->bmax[a], +1));
-        if (dd[a] == 0.0f) {
-            out |= (oo[a] < blo) | (oo[a] > bhi);
-        } else {
-            float t0 = (blo - oo[a]) * inv[a], t1 = (bhi - oo[a]) * inv[a];
-            float a0 = t0 < t1 ? t0 : t1, a1 = t0 < t1 ? t1 : t0;
-            lo = a0 > lo ? a0 : lo;
-            hi = a1 < hi ? a1 : hi;
-        }
+        int neg = signbit(dd[a]) != 0;
+        float t0 = ((neg ? bhi : blo) - oo[a]) * inv[a], t1 = ((neg ? blo : bhi) - oo[a]) * inv[a];
+        lo = t0 > lo ? t0 : lo;
+        hi = t1 < hi ? t1 : hi;
     }
-    return !out && !(lo * KD_EPS_LO > hi * KD_EPS_HI);
+    return !(lo * KD_EPS_LO > hi * KD_EPS_HI);
 }
 
 static hit_t isect_kd_ordered(qctx* q, orc_v3 o, orc_v3 d) {

@@ -9,8 +9,9 @@
 # Every GPU step has its own time limit; the first failure ends the script.
 set -e
 R=$PWD
-O=${OUT:-$R/gpurun_out/r06}
+O=${OUT:-gpurun_out/r06}
 mkdir -p $O
+O=$(cd $O && pwd)
 export OUT=$O TMPDIR=/tmp
 [ -n "$SKIP_CHECK" ] || bash scripts/gpu_check.sh
 for kb in reference sah; do
@@ -25,3 +26,5 @@ for sc in scene01 cornell_bunny70k; do
   grep -h "mcpt lane use\|mcpt phase" $O/phase_$sc.log | tail -2
 done
 echo phase done
+# A/B: the sign-ordered child-box test (MCPT_BOX_SIGN=1, libmcpt_box.so) on C4
+LIBS="libmcpt.so libmcpt_box.so" ROUNDS=${AB_ROUNDS:-2} STEPS=10 NOTEST=1 NOPMC=1 OUT=$O/ab_box bash scripts/ab_c4.sh
