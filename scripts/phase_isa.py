@@ -91,6 +91,7 @@ def regions(ins):
             guard_end.append(tgt)
         if cur is not None:
             cnt[klass(txt) + ("_c" if guard_end else "")] += 1
+            cnt[klass(txt) + f"_d{min(len(guard_end), 2)}"] += 1
         i += 1
     if cur is not None:
         res[cur].append(cnt)
@@ -114,7 +115,8 @@ def main():
             n = len(copies)
             print(f"  marker {m}: {n} cop{'y' if n == 1 else 'ies'}, per copy: " +
                   " ".join(f"{k} {tot[k] / n:.1f}+{tot[k + '_c'] / n:.1f}" for k in ("valu", "salu", "lds", "vmem")) +
-                  "  (always + inside execz-skippable regions)")
+                  "  (always + inside execz-skippable regions); valu by nesting 0/1/2+: " +
+                  "/".join(f"{tot['valu_d' + str(i)] / n:.1f}" for i in range(3)))
 
 
 if __name__ == "__main__":
