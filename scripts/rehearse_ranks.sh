@@ -3,13 +3,19 @@
 # (gloo for the gather and the timing reductions, as tests/test_gpu_ranks.py at
 # N = 2): the full C2 frame, rank 0's PMC passes included, then rank 0's
 # gathered image against a one-process render of the same frame.
-#   NS="4 8" bash scripts/rehearse_ranks.sh
+#   NS="4 8" [SELF=1] bash scripts/rehearse_ranks.sh
+# SELF=1: no launcher -- `bench.py --gpus N` starts its own torch.distributed.run
 set -e
 mkdir -p gpurun_out/rehearse
 for n in ${NS:-4 8}; do
-  MCPT_DIST_BACKEND=gloo MASTER_ADDR=127.0.0.1 timeout -k 10 500 python -m torch.distributed.run --nnodes=1 \
-    --nproc-per-node $n --master-addr 127.0.0.1 --master-port $((29500 + n)) bench.py --gpus $n --steps 2 --warmup 1 \
-    --no-cpu-baseline --dump-image gpurun_out/rehearse/img_n$n.npy > gpurun_out/rehearse/n$n.log 2>&1
+  if [ -n "$SELF" ]; then
+    MCPT_DIST_BACKEND=gloo timeout -k 10 500 python bench.py --gpus $n --steps 2 --warmup 1 \
+      --no-cpu-baseline --dump-image gpurun_out/rehearse/img_n$n.npy > gpurun_out/rehearse/n$n.log 2>&1
+  else
+    MCPT_DIST_BACKEND=gloo MASTER_ADDR=127.0.0.1 timeout -k 10 500 python -m torch.distributed.run --nnodes=1 \
+      --nproc-per-node $n --master-addr 127.0.0.1 --master-port $((29500 + n)) bench.py --gpus $n --steps 2 --warmup 1 \
+      --no-cpu-baseline --dump-image gpurun_out/rehearse/img_n$n.npy > gpurun_out/rehearse/n$n.log 2>&1
+  fi
   grep '^{' gpurun_out/rehearse/n$n.log > gpurun_out/rehearse/n$n.jsonl
 done
 timeout -k 10 300 python - <<'PY'
