@@ -137,3 +137,16 @@ def test_bench_refuses_world_size_mismatch():
     assert r.returncode != 0 and "WORLD_SIZE=3" in r.stderr, r.stderr[-2000:]
     r = _run_bench(["--gpus", "1", "--steps", "1"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr, r.stderr[-2000:]
+
+
+def test_pmc_child_replays_the_line_s_scene_options():
+    """The PMC passes profile the same render as the line: the child's argument
+    list carries the KD split rule and the material sort (bench._workload_args)."""
+    import argparse
+    bench = _bench()
+    a = argparse.Namespace(scene="scene01", width=64, height=48, spp=4, spp_chunk=2, pipeline="wavefront",
+                           wf_batch=0, wf_streams=0, layout="auto", set=[], counting=False, wf_sort=True,
+                           kd_build="sah")
+    w = bench._workload_args(a, (2, 1))
+    assert w[w.index("--kd-build") + 1] == "sah" and "--wf-sort" in w
+    assert w[w.index("--pmc-shard") + 1] == "2,1"
