@@ -473,6 +473,24 @@ def launch_ranks(args, argv: list) -> int:
     return subprocess.run(cmd, env=env).returncode
 
 
+def finish_ranks(dist, rank: int, datetime) -> None:
+    """Hold ranks 1..N-1 until rank 0 has printed its line, then tear down
+    together.  Rank 0's untimed work after the timing (the PMC child processes)
+    takes a minute or more; a rank waiting for it inside a collective would hit
+    the process group's timeout, and a rank shutting its communicator down
+    alone may block in a finalize its peers do not join -- either way the
+    launcher ends every rank, rank 0's line included.  The wait is on the
+    rendezvous store, which has no watchdog (MCPT_DIST_FINISH_S, default 1200 s),
+    and the closing barrier finds every rank present."""
+    store = dist.distributed_c10d._get_default_store()
+    if rank == 0:
+        store.set("mcpt_bench_line_done", "1")
+    else:
+        store.wait(["mcpt_bench_line_done"],
+                   datetime.timedelta(seconds=int(os.environ.get("MCPT_DIST_FINISH_S", "1200"))))
+    dist.barrier()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -850,6 +868,7 @@ def main():
                                                 args.cpu_threads or host_cores(), c1["rays"])
         print(json.dumps(line), flush=True)
     if world > 1:
+        finish_ranks(dist, rank, datetime)
         dist.destroy_process_group()
 
 
