@@ -57,23 +57,21 @@ def algorithmic_bytes(st: dict, pixels: int) -> dict:
     return {"survey": survey, "own": own}
 
 
-def ray_stream_bytes(rays: float, paths: float, variant: int, sort: bool = False, qe: bool = False) -> float:
+def ray_stream_bytes(rays: float, paths: float, variant: int, qe: bool = False) -> float:
     """Bytes of ray stream the extend reads per frame (wavefront.hip implicit0 /
     the packet bounce 0): later bounces read 32 B per ray (origin + direction).
-    Bounce 0 in CV mode with the queue-order shade reads 16 B per path (the
-    direction; the origin is the eye), and nothing on the LDS wavefront (kernel
-    variant 4), whose bounce-0 packet extend computes the primary rays itself
-    (MCPT_WF_GEN0); with the material sort or in QuinEngine mode (near-plane
-    origins) bounce 0 reads both streams, 32 B per path."""
-    implicit0 = not sort and not qe
-    b0 = (0.0 if variant == 4 else 16.0) if implicit0 else 32.0
+    Bounce 0 in CV mode reads 16 B per path (the direction; the origin is the
+    eye), and nothing on the LDS wavefront (kernel variant 4), whose bounce-0
+    packet extend computes the primary rays itself (MCPT_WF_GEN0); in
+    QuinEngine mode (near-plane origins) bounce 0 reads both streams, 32 B per
+    path.  The material sort (wf_sort) sorts inside the shade: same streams."""
+    b0 = 32.0 if qe else (0.0 if variant == 4 else 16.0)
     return b0 * paths + 32.0 * (rays - paths)
 
 
-def hit_write_bytes(rays: float, sort: bool = False) -> float:
-    """The extend's hit stream: the 4-B triangle id per ray in queue order, the
-    16-B hit record {t, beta, gamma, id} under the material sort."""
-    return (16.0 if sort else 4.0) * rays
+def hit_write_bytes(rays: float) -> float:
+    """The extend's hit stream: the 4-B triangle id per ray."""
+    return 4.0 * rays
 
 
 def _workload_args(args, shard=(1, 0)) -> list:
@@ -417,8 +415,8 @@ def c4_line(args) -> dict:
 def c5_line(args) -> dict:
     """BASELINE configs[4] (C5: the wavefront pipeline at 4096 spp -- per-bounce
     compaction of live rays into the next queue; the shade runs in queue order,
-    the material-sorted shade (wf_sort = 1) renders the same image slower,
-    DESIGN.md 5b) on ONE GPU: configs[4] names 8 GPUs, which the driver's
+    the material-sorted shade (wf_sort = 1, the c5_sorted line) renders the
+    same image) on ONE GPU: configs[4] names 8 GPUs, which the driver's
     node runs as the main line's N = 8 shares; 3-5 steps (a step is ~1 s)."""
     line = child_line(args, "scene01", 4 * args.spp, max(3, min(args.steps, 5)), 1, "c5")
     if "config" in line:
@@ -437,12 +435,13 @@ def c2_sah_line(args) -> dict:
 
 def c5_sorted_line(args) -> dict:
     """BASELINE configs[4] as it is worded -- per-bounce compaction PLUS the
-    material sort (wf_sort = 1: extend appends each hit to its material's class
-    list, shade reads the classes in turn) -- on one GPU, 3 steps, no PMC
-    passes (the same image as the c5 line, bit for bit)."""
+    material sort (wf_sort = 1: the shade counting-sorts each block of its queue
+    by material in LDS, so a wave runs one material branch) -- on one GPU, 3
+    steps, no PMC passes (its extend is the c5 line's; the same image as the
+    c5 line, bit for bit)."""
     line = child_line(args, "scene01", 4 * args.spp, 3, 1, "c5_sorted", extra=("--wf-sort", "--no-pmc"))
     if "config" in line:
-        line["config"]["shade"] = "material-sorted (wf_sort=1: per-bounce compaction + class lists)"
+        line["config"]["shade"] = "material-sorted (wf_sort=1: per-bounce compaction + per-block LDS sort by material)"
     return line
 
 
@@ -740,11 +739,11 @@ def main():
                     # the extend's ray stream (ray_stream_bytes) against the exact fabric reads: the rest
                     # is node / triangle records (and stack refills) fetched past the L2
                     shard_rays, shard_paths = per_launch["rays"] / n_gpus, per_launch["paths"] / n_gpus
-                    ray_gb = ray_stream_bytes(shard_rays, shard_paths, st["variant"], sort=args.wf_sort) / 1e9
+                    ray_gb = ray_stream_bytes(shard_rays, shard_paths, st["variant"]) / 1e9
                     roof["read_split"] = {
                         "exact_read_GB": rr["exact_read_GB"], "fetch_size_factor": rr["fetch_size_factor"],
                         "ray_GB": round(ray_gb, 3), "record_GB": round(rr["exact_read_GB"] - ray_gb, 3),
-                        "hit_id_write_GB": round(hit_write_bytes(shard_rays, args.wf_sort) / 1e9, 3),
+                        "hit_id_write_GB": round(hit_write_bytes(shard_rays) / 1e9, 3),
                         "spill_write_GB": round(16.0 * per_launch["stack_spills"] / n_gpus / 1e9, 3),
                         "method": "TCC_EA0_RDREQ_{32B,64B,128B} pass: exact = 32 n32 + 64 n64 + 128 n128 (every "
                                   "request 128 B here; FETCH_SIZE counts 64 B each, factor 2 exactly, "

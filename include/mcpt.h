@@ -100,9 +100,9 @@ typedef struct {
                                    rays, paths and shades stay).  The counts are deterministic:
                                    a counting render of the same params reports what a lean one
                                    did.  0 (default): count everything */
-    int32_t wf_sort;            /* wavefront: 1 = material sort (extend files each finished ray in
-                                   its material's list, shade runs one material per wave over
-                                   the lists); 0 (default) = shade in queue order (dense reads,
+    int32_t wf_sort;            /* wavefront: 1 = material sort (shade sorts each block of its
+                                   queue by material in LDS, so a wave runs one material
+                                   branch); 0 (default) = shade in queue order (dense reads,
                                    faster); same image */
     /* Scheduling.  None of these changes the image or the counters, only the
      * time; 0 = automatic (the measured defaults).
@@ -332,7 +332,7 @@ int mcpt_intersect(mcpt_scene* s, int64_t n, const float* o, const float* d, flo
  * (required before hipGraph capture).  Megakernel workspace per render:
  * partial sums 16 B x pixels x ceil(spp/chunk), the tail-split buffer (16 B
  * per sample of the last ~4 units per lane) and the stack spill area (32 x
- * 16 B per lane); wavefront: 120 B per path of the batch (160 with wf_sort).
+ * 16 B per lane); wavefront: 120 B per path of the batch.
  * After a reserve, a render on a CAPTURING stream that needs more than the
  * scene holds fails with MCPT_E_NOMEM before any launch; a render on a
  * non-capturing stream grows the workspace, and the buffers it outgrows are

@@ -502,11 +502,10 @@ int wavefront_streams(const mcpt_scene& s, uint64_t work, const mcpt_render_para
 
 // Device memory of one stream's wavefront workspace for batches of `cap`
 // paths (prepare_wavefront carves it): two ray queues, radiance, per-bounce
-// counters; the material sort also four class lists.  A queue is three float4
-// streams (origin + path id, direction + depth, throughput + RNG state) and
-// the hit stream: 4-B triangle ids in queue order (wavefront.hip kQHIT), 16-B
-// hit records for the material sort.  Queue order: 3 x 16 + 4 B per slot and
-// queue, 120 B per path with the radiance (the sort: 160 B).  Segments hold
+// counters.  A queue is three float4 streams (origin + path id, direction +
+// depth, throughput + RNG state) and the hit stream of 4-B triangle ids
+// (wavefront.hip kQHIT): 3 x 16 + 4 B per slot and queue, 120 B per path with
+// the radiance (the material sort too: it sorts in LDS).  Segments hold
 // whole path groups (2^group_shift paths: 64 for LDS scenes, up to 2^14 for
 // global-memory ones): up to one group of slots per segment beyond the paths.
 struct WfLayout {
@@ -521,8 +520,8 @@ WfLayout wf_layout(const mcpt_scene& s, const Plan& pl, uint64_t cap) {
     WfLayout l;
     l.cap_slots = size_t(cap) + (nseg << pl.wf_group_shift);
     l.f4 = l.cap_slots * 16;
-    l.queue = al256(pl.wf_sort ? 4 * l.f4 : 3 * l.f4 + 4 * l.cap_slots);
-    l.need = al256(2 * l.queue + l.f4 + (pl.wf_sort ? 4 * l.cap_slots * 4 : 0) + bounces * sizeof(mcpt::WfCounters) + 256);
+    l.queue = al256(3 * l.f4 + 4 * l.cap_slots);
+    l.need = al256(2 * l.queue + l.f4 + bounces * sizeof(mcpt::WfCounters) + 256);
     return l;
 }
 
@@ -774,10 +773,6 @@ void prepare_wavefront(mcpt_scene& s, const Plan& pl, int sets, mcpt::WfParams* 
         w.q[0] = reinterpret_cast<float4*>(b); b += l.queue;
         w.q[1] = reinterpret_cast<float4*>(b); b += l.queue;
         w.radiance = reinterpret_cast<float4*>(b); b += l.f4;
-        if (pl.wf_sort) {
-            w.cls_list = reinterpret_cast<uint32_t*>(b);
-            b += 4 * l.cap_slots * 4;
-        }
         w.cnt = reinterpret_cast<mcpt::WfCounters*>(b);
         w.capacity = pl.wf_capacity;                   // paths per batch (pid range)
         w.slot_stride = static_cast<uint32_t>(l.cap_slots);

@@ -148,24 +148,23 @@ struct QueryParams {
 // [s_begin, s_begin + ns) of chunk `chunk` for owned pixels [v0, v0 + nb);
 // path id pid = s_local * nb + (v - v0).  The batch is cut into `nseg`
 // segments of `seg` paths, one per extend workgroup; a path stays in its
-// segment for all bounces, so each segment's queues, class lists and
-// counters are private to one workgroup (LDS atomics only).  Queue slot j of
+// segment for all bounces, so each segment's queues and counters are private
+// to one workgroup (LDS atomics only).  Queue slot j of
 // segment g is entry g*seg + j; path state and radiance are indexed by pid.
 struct WfCounters {                      // per (bounce, segment), 8 words
-    uint32_t queued;                     // rays in this segment's queue
-    uint32_t cls[4];                     // class-list lengths after extend
-    uint32_t pad[3];
+    uint32_t queued;                     // rays in this segment's queue (written by its producer)
+    uint32_t hits;                       // slots whose hit id extend wrote (= queued; shade's count)
+    uint32_t pad[6];
 };
 struct WfParams {
-    // ray queue b: four float4 streams of slot_stride entries (SoA):
-    // {o.xyz pid} {d.xyz depth} {t beta gamma htri} {throughput.xyz rng};
-    // extend reads streams 0-1 and writes stream 2, shade reads all four
-    float4* q[2];                        // [4][slot_stride]
-    uint32_t* cls_list;                  // [4][capacity] slots per material class
+    // ray queue b: three float4 streams of slot_stride entries (SoA),
+    // {o.xyz pid} {d.xyz depth} {throughput.xyz rng}, then the 4-B hit ids;
+    // extend reads streams 0-1 and writes the ids, shade reads all four
+    float4* q[2];
     float4* radiance;                    // path radiance per pid                   [capacity]
     WfCounters* cnt;                     // [max_depth + 2][nseg]
     uint32_t capacity;                   // paths per batch
-    uint32_t slot_stride;                // queue / class-list entries per array (>= nseg * seg)
+    uint32_t slot_stride;                // queue entries per stream (>= nseg * seg)
     uint32_t v0, nb, s_begin, ns, chunk_index;   // pixels [v0, v0+nb) x samples [s_begin, s_begin+ns)
     uint32_t nsc;                        // samples per chunk (ns = whole chunks of nsc)
     uint32_t nseg, seg;                  // segments (= extend workgroups) and slots per segment
@@ -173,7 +172,7 @@ struct WfParams {
                                          // (the plan's for global-memory scenes; 6 in LDS)
     int32_t bounce;
     int32_t refill_thresh;               // idle lanes before an extend wave refills
-    int32_t sort;                        // 1: material sort (class lists), 0: shade in queue order
+    int32_t sort;                        // 1: shade sorts each block of slots by material first
     uint32_t xcd_deal;                   // 1: groups dealt to segments by XCD (global-memory scenes, seg_of)
 };
 

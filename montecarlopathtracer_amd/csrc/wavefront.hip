@@ -13,15 +13,13 @@
 //               per queue segment, scene image in LDS (or global); waves
 //               reserve slots 64 at a time from an LDS counter, each lane
 //               prefetches its next ray while tracing the current one and
-//               refills as soon as it is done; the slot then goes to one of
-//               four per-class lists (terminate / diffuse / phong / fresnel) --
-//               the material sort of the extend -> shade hand-off -- buffered
-//               64 entries per class in registers (ds_permute) and written as
-//               one coalesced block per LDS atomic
-//   shade b     each segment's class lists back to back, so each wave runs ONE
-//               material branch: radiance of terminated paths, or the scatter
-//               event whose next ray goes to slot i of the segment's queue b+1
-//               (dense, no atomics)
+//               refills as soon as it is done; it writes the slot's hit id
+//   shade b     each segment's queue b in blocks of slots: radiance of
+//               terminated paths, or the scatter event whose next ray goes to
+//               the next free slot of the segment's queue b+1 (per-bounce
+//               compaction by one LDS atomic per wave); with the material sort
+//               (wf_sort = 1) each block is first sorted by material in LDS, so
+//               a wave runs one material branch
 //   accumulate  per pixel, the batch's samples summed in sample order into the
 //               same [chunk][pixel] partial sums the megakernel writes
 // followed by the megakernel's reduction.  A path never leaves its segment,
@@ -58,7 +56,6 @@ using namespace trace;
 namespace {
 
 constexpr int kGenBlock = 256;
-constexpr int kShadeBlock = 256;
 constexpr int kClassTerminate = 0;
 // Rays are carried as (o.xyz, pid) and (d.xyz, depth); depth kNoRay marks a
 // queue slot without a ray (pixel outside the image): it ends as a miss with
@@ -73,38 +70,32 @@ __device__ __forceinline__ float opaque(float x) {
 __device__ __forceinline__ float4 pack(V3 v, uint32_t w) { return make_float4(v.x, v.y, v.z, __uint_as_float(w)); }
 
 // Queue layout: field k of slot j (kQO {o, pid}, kQD {d, depth}, kQPS
-// {throughput, rng}, kQHIT hit {t, beta, gamma, htri} or the 4-B id), four
-// SoA float4 streams of slot_stride entries each -- extend's ray reads and hit
-// writes are dense lane streams (64-B AoS records: generate 9 -> 33 ms per C2
-// frame, round 2).
-// WfParams::sort (mcpt_render_params::wf_sort) -- material sort (1): extend
-// appends each finished slot to its segment's class list and shade gathers
-// the records list by list (one material per wave).  Queue order (0, default):
-// shade reads its segment's queue in slot order -- dense streams, no class
-// lists, the merged samplers absorb the material mix -- and appends continuing
-// rays to the next queue with one LDS atomic per wave (C2 wavefront 7.56 ->
-// 10.03 G rays/s: the sorted shade's gathers cost more than the divergence).
+// {throughput, rng}: SoA float4 streams of slot_stride entries each, then
+// kQHIT, the 4-B hit ids) -- extend's ray reads and hit writes are dense lane
+// streams (64-B AoS records: generate 9 -> 33 ms per C2 frame, round 2).
+// WfParams::sort (mcpt_render_params::wf_sort): 0 (default) -- shade takes its
+// segment's queue in slot order, dense streams, the merged samplers absorbing
+// the material mix; 1 -- shade sorts each block of slots by material first
+// (wf_shade_slots SORTB).  Either way continuing rays go to the next queue
+// with one LDS atomic per wave.  (Until round 6 the sort went through
+// per-class slot lists that extend appended to and shade gathered from: 9.5
+// against 13.6 G rays/s for the block sort on C2, PERFLOG row 156.)
 __device__ __forceinline__ size_t qf(uint32_t slot, uint32_t k, uint32_t stride) {
     return (size_t)k * stride + slot;
 }
 // queue streams: origin + path id, direction + depth, throughput + RNG state,
-// hit (last: in queue order it holds only 4-B triangle ids, so the queue is
-// 3 x 16 + 4 B per slot; the material sort keeps 16-B hit records)
+// hit (last: it holds only 4-B triangle ids, so the queue is 3 x 16 + 4 B per
+// slot)
 constexpr uint32_t kQO = 0, kQD = 1, kQPS = 2, kQHIT = 3;
 __device__ __forceinline__ V3 xyz(float4 v) { return v3(v.x, v.y, v.z); }
 
 // Queue streams are touched once per bounce: MCPT_WF_NT marks the streaming
 // reads (bit 0) and writes (bit 1) of generate, shade and extend's ray reads
-// (bit 2: also extend's hit writes) non-temporal, so that they do not push
-// extend's partially written hit lines out of the L2.  Default 3 (C2
-// wavefront +3.5%, C4 +2%; with bit 2 as well: C2 +2%, C4 +2.8%).
+// non-temporal, so that they do not push extend's partially written hit lines
+// out of the L2.  Default 3 (C2 wavefront +3.5%, C4 +2%; the 4-B hit ids
+// themselves are plain stores, PERFLOG row 79).
 #ifndef MCPT_WF_NT
 #define MCPT_WF_NT 3
-#endif
-// extend's hit writes non-temporal for scenes in global memory only (C4
-// wavefront +0.9%, two rounds)
-#ifndef MCPT_WF_NT_HIT_GLOBAL
-#define MCPT_WF_NT_HIT_GLOBAL 1
 #endif
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ float4 ldq(const float4* p) {
@@ -114,10 +105,6 @@ __device__ __forceinline__ float4 ldq(const float4* p) {
 #else
     return *p;
 #endif
-}
-__device__ __forceinline__ void stq_nt(float4* p, float4 v) {
-    const f32x4 x = {v.x, v.y, v.z, v.w};
-    __builtin_nontemporal_store(x, reinterpret_cast<f32x4*>(p));
 }
 __device__ __forceinline__ void stq(float4* p, float4 v) {
 #if MCPT_WF_NT & 2
@@ -188,9 +175,9 @@ __device__ __forceinline__ uint32_t seg_queue0_len(const WfParams& wf, uint32_t 
 #define MCPT_WF_IMPLICIT0 2
 #endif
 __host__ __device__ __forceinline__ bool implicit0(const KernelParams& kp, const WfParams& wf) {
-    return MCPT_WF_IMPLICIT0 && !wf.sort && kp.mode != kModeQE;
+    return MCPT_WF_IMPLICIT0 && kp.mode != kModeQE;
 }
-// Hit ids (queue order): extend writes only the hit triangle's id (4 B, the
+// Hit ids: extend writes only the hit triangle's id (4 B, the
 // first quarter of the hit stream as i32) and shade recomputes t, beta, gamma
 // of a scattering ray from it (tri_hit_params: the traversal's own
 // operations, bit-identical).  The 16-B hit records cost the extend 2.4x their
@@ -238,49 +225,6 @@ __global__ void __launch_bounds__(kGenBlock) wf_generate(const KernelParams kp, 
     flush_counters(c, kp.stats);
 }
 
-// Per-class output buffer held in registers: lane j holds entry j of the
-// wave's pending 64-entry block; full blocks go out with one LDS atomic and
-// one coalesced store.  Entries move to their lane with ds_permute (all 64
-// lanes send: appenders to the new positions, the others to the remaining
-// lanes, so the permutation has no collisions).
-struct ClassBuf {
-    uint32_t val, count;
-    __device__ __forceinline__ void append(bool want, uint32_t x, uint32_t* counter, uint32_t* list) {
-        const uint64_t m = __ballot(want);
-        const uint32_t n = (uint32_t)__popcll(m);
-        if (n == 0) return;                           // wave-uniform
-        const int lane = (int)(threadIdx.x & 63u);
-        const uint64_t lt = (1ull << lane) - 1ull;
-        const uint32_t pos = want ? (uint32_t)__popcll(m & lt) : n + (uint32_t)__popcll(~m & lt);
-        const uint32_t dst = (count + pos) & 63u;
-        const uint32_t recv = (uint32_t)__builtin_amdgcn_ds_permute((int)(dst << 2), (int)x);
-        const uint32_t off = ((uint32_t)lane - count) & 63u;
-        const bool mine = off < n;
-        const uint32_t hi = count + n;
-        if (hi < kChunk) {
-            if (mine) val = recv;
-            count = hi;
-        } else {
-            if (mine && (uint32_t)lane >= count) val = recv;
-            uint32_t b = 0;
-            if (lane == 0) b = atomicAdd(counter, kChunk);
-            b = lane_bcast(b, 0);
-            list[b + (uint32_t)lane] = val;
-            if (mine && (uint32_t)lane < count) val = recv;
-            count = hi - kChunk;
-        }
-    }
-    __device__ __forceinline__ void flush(uint32_t* counter, uint32_t* list) {
-        if (count == 0) return;
-        const int lane = (int)(threadIdx.x & 63u);
-        uint32_t b = 0;
-        if (lane == 0) b = atomicAdd(counter, count);
-        b = lane_bcast(b, 0);
-        if ((uint32_t)lane < count) list[b + (uint32_t)lane] = val;
-        count = 0;
-    }
-};
-
 #endif  // !MCPT_WF_PRIMARY_TU
 
 // Issue priority of the extend's traversal bursts (its hand-off runs one
@@ -305,11 +249,11 @@ constexpr int kWfLdsCap = MCPT_WF_DESCENT_CAP;
 // Workgroups of 256 threads, kGlobalBlocksPerCu per CU per launch; other
 // streams' extends fill further slots as far as LDS and VGPRs allow.
 // MCPT_WF_GLOBAL_S: LDS stack entries per lane; MCPT_WF_GLOBAL_WAVES: waves per
-// SIMD the compiler must allow (its VGPR budget; the lean queue-order kernel
-// only -- the untimed counting kernels and the material sort's class buffers
-// keep their registers) -- with 256-thread workgroups (one wave per SIMD
-// each) that is the resident workgroups per CU.  6 x 6: 80 VGPRs
-// (no scratch) and 6 x 24 KB of LDS, six extend waves per SIMD.  C4 G rays/s:
+// SIMD the compiler must allow (its VGPR budget; the lean kernel only -- the
+// untimed counting kernels keep their registers) -- with 256-thread
+// workgroups (one wave per SIMD each) that is the resident workgroups per CU.
+// 6 x 6: 80 VGPRs (no scratch) and 6 x 24 KB of LDS, six extend waves per
+// SIMD.  C4 G rays/s:
 // S = 8, no hint (round 3: 32 KB, four workgroups, 88 VGPRs) 9.46 / 9.47;
 // S = 6 9.61 / 9.63; S = 7 (five workgroups) 9.85 / 9.87; S = 5 9.20; S = 4
 // 8.78 (spills); S = 6 with six workgroups (80 VGPRs) 10.36 / 10.31.
@@ -345,17 +289,14 @@ constexpr int kLayGlobal = 0, kLayLds = 1;
 #if !MCPT_WF_PRIMARY_TU
 // ---- extend: closest hit of every ray of this workgroup's segment -----------
 // COUNT = false (lean renders): the traversal counters are compiled out.
-// SORT = WfParams::sort, a template argument so that the queue-order variant
-// carries no class-list buffers (8 VGPRs: the co-resident shade of the
-// multi-stream pipeline needs the extend at <= 96)
 // LAY: kLayGlobal (scene image with child-box records in global memory) or
 // kLayLds (the whole 8-B-node image copied into LDS; a hybrid with only the
 // triangle records in L1/L2 and two 768-thread workgroups per CU measured
 // -24%, round 4)
-template <int LAY, int S, int BLOCK, bool COUNT, bool SORT>
-__global__ void __launch_bounds__(BLOCK, (LAY == kLayGlobal && !COUNT && !SORT && MCPT_WF_GLOBAL_WAVES)
+template <int LAY, int S, int BLOCK, bool COUNT>
+__global__ void __launch_bounds__(BLOCK, (LAY == kLayGlobal && !COUNT && MCPT_WF_GLOBAL_WAVES)
                                              ? MCPT_WF_GLOBAL_WAVES
-                                             : (LAY == kLayLds && !COUNT && !SORT && MCPT_WF_LDS_WPE
+                                             : (LAY == kLayLds && !COUNT && MCPT_WF_LDS_WPE
                                                     ? MCPT_WF_LDS_WPE : 1))   // (waves per SIMD)
 wf_extend(const KernelParams kp, const WfParams wf) {
     constexpr bool IN_LDS = LAY != kLayGlobal;            // node words in LDS
@@ -364,19 +305,18 @@ wf_extend(const KernelParams kp, const WfParams wf) {
     WfCounters* cn = wf.cnt + (size_t)wf.bounce * wf.nseg + g;
     const uint32_t count = g < wf.nseg ? cn->queued : 0u;
     if (count == 0) {
-        if (g < wf.nseg && threadIdx.x < 4) cn->cls[threadIdx.x] = 0;
+        if (g < wf.nseg && threadIdx.x == 0) cn->hits = 0;
         return;
     }
     const int tid = (int)threadIdx.x;
     const GpuScene& sc = kp.scene;
-    // LDS: [stack S x BLOCK x 16 B | scene image (kLayLds) | 5 counters]
+    // LDS: [stack S x BLOCK x 16 B | scene image (kLayLds) | slot counter]
     unsigned char* const lds_image = smem + (size_t)S * BLOCK * 16;
-    uint32_t* lcnt = reinterpret_cast<uint32_t*>(lds_image + (IN_LDS ? sc.image_bytes : 0u));
-    if (tid < 5) lcnt[tid] = 0;
+    uint32_t* const lslot = reinterpret_cast<uint32_t*>(lds_image + (IN_LDS ? sc.image_bytes : 0u));
+    if (tid == 0) *lslot = 0;
     const float4* tris;
     const uint2* nodes;
     const uint32_t* leafs;
-    const GpuGeom* geoms;
     if constexpr (IN_LDS) {
         const uint4* src = reinterpret_cast<const uint4*>(sc.image);
         uint4* dst = reinterpret_cast<uint4*>(lds_image);
@@ -385,12 +325,10 @@ wf_extend(const KernelParams kp, const WfParams wf) {
         tris = reinterpret_cast<const float4*>(lds_image + sc.off_tris);
         nodes = reinterpret_cast<const uint2*>(lds_image + sc.off_nodes) + 1;
         leafs = reinterpret_cast<const uint32_t*>(lds_image + sc.off_leafs);
-        geoms = reinterpret_cast<const GpuGeom*>(lds_image + sc.off_geoms);
     } else {
         tris = reinterpret_cast<const float4*>(sc.image + sc.off_tris);
         nodes = reinterpret_cast<const uint2*>(sc.image + sc.off_nodes) + 1;
         leafs = reinterpret_cast<const uint32_t*>(sc.image + sc.off_leafs);
-        geoms = reinterpret_cast<const GpuGeom*>(sc.image + sc.off_geoms);
     }
     const uint4* pairs = reinterpret_cast<const uint4*>(sc.image + sc.off_nodes);   // 48-B pair records (global variant)
     __syncthreads();
@@ -406,7 +344,6 @@ wf_extend(const KernelParams kp, const WfParams wf) {
     LaneUse lu = {0, 0, 0, 0, 0, 0};
 #endif
     SlotCursor cur_chunk = {0, kChunk};
-    ClassBuf out[4] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
     RayState r;
     r.htri = -1;
     int mode = kDead;
@@ -414,8 +351,8 @@ wf_extend(const KernelParams kp, const WfParams wf) {
     // without it (MCPT_WF_GLOBAL_PREFETCH = 0, global-memory scenes only) a
     // finished lane loads its next ray in the hand-off, 8 VGPRs fewer
     constexpr bool PF = LAY != kLayGlobal || MCPT_WF_GLOBAL_PREFETCH;
-    uint32_t slot = cur_chunk.take(true, lcnt + 4), depth = 0;
-    uint32_t nslot = PF ? cur_chunk.take(true, lcnt + 4) : 0u;
+    uint32_t slot = cur_chunk.take(true, lslot), depth = 0;
+    uint32_t nslot = PF ? cur_chunk.take(true, lslot) : 0u;
     float4 no4 = make_float4(0, 0, 0, 0), nd4 = make_float4(0, 0, 0, 0);
     auto start = [&](float4 o4, float4 d4) {
         // opaque copies: the loop below must not see its ray registers as
@@ -475,7 +412,7 @@ wf_extend(const KernelParams kp, const WfParams wf) {
 #ifdef MCPT_PHASE_TIMING
         tm_hands++;
 #endif
-        // ---- hand-off: hit record + per-material class list -----------------
+        // ---- hand-off: hit id, next ray -----------------------------------
         MCPT_MARK(7);
         __builtin_amdgcn_s_setprio(MCPT_WF_EXT_PRIO + 1);   // as the megakernel's shading rounds: short phase, raised priority
         // Settle the prefetch (issued a whole burst ago) before any store of
@@ -490,20 +427,10 @@ wf_extend(const KernelParams kp, const WfParams wf) {
             nd4 = make_float4(opaque(nd4.x), opaque(nd4.y), opaque(nd4.z), opaque(nd4.w));
         }
         const bool fin = mode == kReady;
-        const uint32_t ns0 = PF ? 0u : cur_chunk.take(fin, lcnt + 4);   // (collective: every lane)
-        uint32_t cls = 4u;
+        const uint32_t ns0 = PF ? 0u : cur_chunk.take(fin, lslot);   // (collective: every lane)
         const uint32_t fslot = slot;
-        float4 hrec = make_float4(0, 0, 0, 0);
         if (fin) {
-            hrec = make_float4(r.best, r.hbeta, r.hgamma, __int_as_float(r.htri));
-            cls = kClassTerminate;
-            // CV: scatter while depth < max_depth (CUTracer.cu:103-160); QE: while
-            // bounce < 3*depth (rtx.hlsl:312), roulette is drawn in shade
-            const int32_t lim = kp.mode == kModeQE ? 3 * kp.max_depth : kp.max_depth;
-            if (SORT && r.htri >= 0 && depth != kNoRay && (int32_t)depth < lim) {
-                const GpuGeom& gm = geoms[__float_as_uint(tris[r.htri + 1].w)];
-                if (!is_emitter(gm)) cls = material_class(gm);
-            }
+            const int32_t hid = r.htri;
             // (the next ray set up unconditionally: no branch in the hand-off; a
             // lane past the segment's end runs on its stale prefetch, then dies)
             if constexpr (PF) {
@@ -516,22 +443,13 @@ wf_extend(const KernelParams kp, const WfParams wf) {
                 start(o4, d4);
             }
             if (slot >= count) mode = kDead;
-            if constexpr (!SORT)   // (r holds the next ray by now: the id from hrec)
-                reinterpret_cast<int32_t*>(qb + qf(0, kQHIT, qs))[seg0 + fslot] = __float_as_int(hrec.w);
-            else if constexpr ((MCPT_WF_NT & 4) != 0 || (!IN_LDS && MCPT_WF_NT_HIT_GLOBAL))
-                stq_nt(&qb[qf(seg0 + fslot, kQHIT, qs)], hrec);
-            else
-                qb[qf(seg0 + fslot, kQHIT, qs)] = hrec;
-        }
-        if constexpr (SORT) {
-#pragma unroll
-            for (uint32_t k = 0; k < 4; k++)
-                out[k].append(cls == k, fslot, lcnt + k, wf.cls_list + (size_t)k * wf.slot_stride + seg0);
+            // (r holds the next ray by now: the id saved before)
+            reinterpret_cast<int32_t*>(qb + qf(0, kQHIT, qs))[seg0 + fslot] = hid;
         }
         // ---- prefetch the next ray of every lane that just started one -------
         if constexpr (PF) {
             const bool want = fin && mode != kDead;
-            const uint32_t ns = cur_chunk.take(want, lcnt + 4);
+            const uint32_t ns = cur_chunk.take(want, lslot);
             if (want) {
                 nslot = ns;
                 if (nslot < count) { no4 = ld_o(nslot); nd4 = ldq(&qb[qf(seg0 + nslot, kQD, qs)]); }
@@ -540,10 +458,6 @@ wf_extend(const KernelParams kp, const WfParams wf) {
         WF_STAMP(tm_hand);
         MCPT_MARK(8);
         if (!__ballot(mode != kDead)) break;
-    }
-    if constexpr (SORT) {
-#pragma unroll
-        for (uint32_t k = 0; k < 4; k++) out[k].flush(lcnt + k, wf.cls_list + (size_t)k * wf.slot_stride + seg0);
     }
 #ifdef MCPT_PHASE_TIMING
     if ((threadIdx.x & 63u) == 0) {
@@ -564,8 +478,7 @@ wf_extend(const KernelParams kp, const WfParams wf) {
     }
 #endif
     flush_counters(c, kp.stats);
-    __syncthreads();
-    if (tid < 4) cn->cls[tid] = lcnt[tid];
+    if (tid == 0) cn->hits = count;                        // every slot's hit id is written
 }
 
 #endif  // !MCPT_WF_PRIMARY_TU
@@ -616,7 +529,7 @@ __global__ void __launch_bounds__(BLOCK, 1) wf_extend_primary(const KernelParams
         }
     }
     if (count == 0) {
-        if (g < wf.nseg && threadIdx.x < 4) cn->cls[threadIdx.x] = 0;
+        if (g < wf.nseg && threadIdx.x == 0) cn->hits = 0;
         return;
     }
     const int tid = (int)threadIdx.x;
@@ -837,98 +750,34 @@ __global__ void __launch_bounds__(BLOCK, 1) wf_extend_primary(const KernelParams
     }
     if (pslot < count) hq[pslot] = phit;
     flush_counters(c, kp.stats);
-    __syncthreads();
-    if (tid < 4) cn->cls[tid] = 0;
+    if (tid == 0) cn->hits = count;
 }
 
 #if !MCPT_WF_PRIMARY_TU
-// ---- shade: each segment's class lists back to back (CUTracer.cu:105-175) ---
-// Items of segment g are taken in the order [diffuse, phong, fresnel,
-// terminate]; the i-th continuing item writes its next ray to slot i of the
-// segment's queue b+1 (no atomics), so consecutive waves shade one material.
-// `per` workgroups share a segment, each a contiguous share of its items.
-__global__ void __launch_bounds__(kShadeBlock) wf_shade(const KernelParams kp, const WfParams wf, uint32_t per) {
-    const uint32_t g = blockIdx.x / per, q = blockIdx.x - g * per;
-    if (g >= wf.nseg) return;
-    const WfCounters* cn = wf.cnt + (size_t)wf.bounce * wf.nseg + g;
-    WfCounters* nx = wf.cnt + (size_t)(wf.bounce + 1) * wf.nseg + g;
-    const GpuScene& sc = kp.scene;
-    const float4* tris = reinterpret_cast<const float4*>(sc.image + sc.off_tris);
-    const GpuGeom* geoms = reinterpret_cast<const GpuGeom*>(sc.image + sc.off_geoms);
-    const size_t seg0 = (size_t)g * wf.seg;
-    const float4* qb = wf.q[wf.bounce & 1];
-    float4* qb2 = wf.q[(wf.bounce + 1) & 1];
-    const uint32_t qs = wf.slot_stride;
-    const uint32_t p1 = cn->cls[1], p2 = p1 + cn->cls[2], p3 = p2 + cn->cls[3], total = p3 + cn->cls[0];
-    if (q == 0 && threadIdx.x == 0) nx->queued = p3;
-    const uint32_t lo = (uint32_t)(((uint64_t)total * q) / per), hi = (uint32_t)(((uint64_t)total * (q + 1)) / per);
-    Counters c = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (uint32_t i = lo + threadIdx.x; i < hi; i += kShadeBlock) {
-        const uint32_t k = i < p1 ? 1u : (i < p2 ? 2u : (i < p3 ? 3u : 0u));
-        const uint32_t start = k == 1u ? 0u : (k == 2u ? p1 : (k == 3u ? p2 : p3));
-        const uint32_t slot = wf.cls_list[(size_t)k * wf.slot_stride + seg0 + (i - start)];
-        const size_t js = seg0 + slot;
-        const float4 o4 = qb[qf(js, kQO, qs)], d4 = qb[qf(js, kQD, qs)], h = qb[qf(js, kQHIT, qs)], ps = qb[qf(js, kQPS, qs)];
-        const uint32_t pid = __float_as_uint(o4.w);
-        const uint32_t depth = __float_as_uint(d4.w);
-        const int32_t htri = __float_as_int(h.w);
-        const bool qe = kp.mode == kModeQE;
-        if (k == kClassTerminate) {
-            // CV: miss -> 0; emitter -> color*Ka*ILLUM (:111-113); terminal query (:162-175)
-            // QE: miss / bounce >= 3*depth -> 0; roulette, then emitter -> color*Ka (rtx.hlsl:312-331)
-            V3 L = v3(0, 0, 0);
-            if (htri >= 0 && depth != kNoRay) {
-                const GpuGeom& gm = geoms[__float_as_uint(tris[htri + 1].w)];
-                if (qe) {
-                    if ((int32_t)depth < 3 * kp.max_depth) {
-                        V3 color = xyz(ps);
-                        uint32_t sd = __float_as_uint(ps.w);
-                        if ((int32_t)depth < kp.max_depth || qe_roulette(sd, color)) L = emitted(color, gm, 1.0f);
-                    }
-                } else if ((int32_t)depth >= kp.max_depth || is_emitter(gm)) {
-                    L = emitted(xyz(ps), gm, kp.illum);
-                }
-            }
-            wf.radiance[pid] = make_float4(L.x, L.y, L.z, 0.0f);
-        } else {
-            V3 color = xyz(ps);
-            uint32_t sd = __float_as_uint(ps.w);
-            const size_t ji = seg0 + i;                     // the whole next record is written
-            if (qe && (int32_t)depth >= kp.max_depth && !qe_roulette(sd, color)) {
-                // killed by the roulette: zero radiance, an empty slot in queue b+1
-                wf.radiance[pid] = make_float4(0, 0, 0, 0);
-                qb2[qf(ji, kQO, qs)] = pack(v3(0, 0, 0), pid);
-                qb2[qf(ji, kQD, qs)] = pack(v3(0, 0, 0), kNoRay);
-                qb2[qf(ji, kQHIT, qs)] = make_float4(0, 0, 0, 0);
-                qb2[qf(ji, kQPS, qs)] = make_float4(0, 0, 0, 0);
-            } else {
-                c.shades++;
-                const GpuGeom& gm = geoms[__float_as_uint(tris[htri + 1].w)];
-                V3 o = xyz(o4), d = xyz(d4);
-                if (qe) scatter<true>(gm, sc.normals, htri, h.y, h.z, h.x, 0, sd, color, o, d);
-                else scatter<false>(gm, sc.normals, htri, h.y, h.z, h.x, kp.fresnel_kd, sd, color, o, d);
-                qb2[qf(ji, kQO, qs)] = pack(o, pid);
-                qb2[qf(ji, kQD, qs)] = pack(d, depth + 1u);
-                qb2[qf(ji, kQPS, qs)] = pack(color, sd);
-                c.rays++;
-            }
-        }
-    }
-    flush_counters(c, kp.stats);
-}
-
-// ---- shade in queue order (wf_sort 0): one workgroup per segment -----------
+// ---- shade: one workgroup per segment, its queue in blocks of slots ---------
 // Reads the segment's queue b as dense streams (o, d, hit, throughput/rng),
 // finishes terminated paths (radiance by path id) and scatters the others; a
 // continuing ray goes to the next free slot of the segment's queue b+1 (one
 // LDS atomic per wave, 64 consecutive slots), so queue b+1 is dense.  Queue
 // order is scheduling-dependent, but nothing reads it (state keyed by pid).
-template <int BLOCK, bool GEO_LDS>
-__global__ void __launch_bounds__(BLOCK, MCPT_WF_SHADE_WPE ? MCPT_WF_SHADE_WPE : 1)
+// SORTB (wf_sort = 1): the material sort, inside the workgroup --
+// each block of BLOCK queue slots is first classified (terminate / diffuse /
+// phong / fresnel: the slot's hit id, depth and material), then counting-sorted
+// by class in LDS (ranks by ballot, one LDS atomic per class and wave), and
+// lane j shades the block's j-th slot in class order, so a wave runs one
+// material branch except at the (at most three) class boundaries of a block.
+// The class is a scheduling key only: every slot runs the same code.
+// (SORTB held at <= 80 VGPRs, the queue-order shade's count: two of its waves
+// per SIMD beside the LDS extend's four)
+template <int BLOCK, bool GEO_LDS, bool SORTB>
+__global__ void __launch_bounds__(BLOCK, SORTB ? 6 : (MCPT_WF_SHADE_WPE ? MCPT_WF_SHADE_WPE : 1))
 wf_shade_slots(const KernelParams kp, const WfParams wf) {
     const uint32_t g = blockIdx.x;
     if (g >= wf.nseg) return;
     __shared__ uint32_t lnext;
+    __shared__ uint32_t lcls[SORTB ? 8 : 1];               // class counts, two sets (alternate blocks)
+    __shared__ uint16_t lperm[SORTB ? BLOCK : 1];          // block position -> slot offset, in class order
+    if (SORTB && threadIdx.x < 8) lcls[threadIdx.x] = 0;
     // the material table in LDS when it fits beside the co-resident extend
     // (GEO_LDS): its fields are read in the branches of the shading chain,
     // each a dependent round trip that LDS serves in a fraction of L2's time
@@ -936,7 +785,7 @@ wf_shade_slots(const KernelParams kp, const WfParams wf) {
     extern __shared__ __attribute__((aligned(16))) GpuGeom lgeo[];
     const WfCounters* cn = wf.cnt + (size_t)wf.bounce * wf.nseg + g;
     WfCounters* nx = wf.cnt + (size_t)(wf.bounce + 1) * wf.nseg + g;
-    const uint32_t total = cn->queued;
+    const uint32_t total = cn->hits;                       // the slots extend b wrote a hit id for
     const GpuScene& sc = kp.scene;
     if (threadIdx.x == 0) lnext = 0;
     if constexpr (GEO_LDS) {
@@ -955,8 +804,41 @@ wf_shade_slots(const KernelParams kp, const WfParams wf) {
     const bool imp = wf.bounce == 0 && implicit0(kp, wf);
     const int lane = (int)(threadIdx.x & 63u);
     Counters c = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t par = 0;
     for (uint32_t base = 0; base < total; base += BLOCK) {      // block-uniform trip count
-        const uint32_t i = base + threadIdx.x;
+        uint32_t i = base + threadIdx.x;
+        if constexpr (SORTB) {
+            uint32_t k = 4u;                                    // past the queue's end: no entry
+            if (i < total) {
+                const size_t js = seg0 + i;
+                const int32_t htri = reinterpret_cast<const int32_t*>(qb + qf(0, kQHIT, qs))[js];
+                const uint32_t depth = imp ? 0u : __float_as_uint(qb[qf(js, kQD, qs)].w);
+                const int32_t lim = qe ? 3 * kp.max_depth : kp.max_depth;
+                k = kClassTerminate;
+                if (htri >= 0 && depth != kNoRay && (int32_t)depth < lim) {
+                    const GpuGeom& gm = geoms[__float_as_uint(tris[htri + 1].w)];
+                    if (!is_emitter(gm)) k = material_class(gm);
+                }
+            }
+            uint32_t* const lc = lcls + 4u * par;
+            const uint64_t m0 = __ballot(k == 0u), m1 = __ballot(k == 1u), m2 = __ballot(k == 2u),
+                           m3 = __ballot(k == 3u);
+            const uint64_t mk = k == 0u ? m0 : k == 1u ? m1 : k == 2u ? m2 : m3;
+            const uint64_t ml = lane == 0 ? m0 : lane == 1 ? m1 : lane == 2 ? m2 : m3;
+            uint32_t off = 0;
+            if (lane < 4) off = atomicAdd(&lc[lane], (uint32_t)__popcll(ml));   // the wave's offset in class `lane`
+            off = (uint32_t)__shfl((int)off, (int)(k & 3u));
+            __syncthreads();
+            // class order in the block: diffuse, phong, fresnel, terminate
+            const uint32_t n1 = lc[1], n2 = lc[2], n3 = lc[3];
+            const uint32_t cb = k == 1u ? 0u : k == 2u ? n1 : k == 3u ? n1 + n2 : n1 + n2 + n3;
+            if (k < 4u) lperm[cb + off + (uint32_t)__popcll(mk & ((1ull << lane) - 1ull))] = (uint16_t)threadIdx.x;
+            if (threadIdx.x < 4) lcls[4u * (par ^ 1u) + threadIdx.x] = 0;
+            __syncthreads();
+            const uint32_t nv = total - base < (uint32_t)BLOCK ? total - base : (uint32_t)BLOCK;
+            if (threadIdx.x < nv) i = base + lperm[threadIdx.x];   // (others: i >= total, no slot)
+            par ^= 1u;
+        }
         bool cont = false;
         uint32_t pid = 0, depth = kNoRay, sd = 0;
         V3 o = v3(0, 0, 0), d = v3(0, 0, 0), color = v3(0, 0, 0);
@@ -1067,13 +949,14 @@ hipError_t launch_extend_primary(const KernelParams& kp, const WfParams& wf, int
 
 #if !MCPT_WF_PRIMARY_TU
 template <int BLOCK>
-auto shade_kernel(bool geo_lds) { return geo_lds ? wf_shade_slots<BLOCK, true> : wf_shade_slots<BLOCK, false>; }
+auto shade_kernel(bool geo_lds, bool sortb) {
+    return sortb ? (geo_lds ? wf_shade_slots<BLOCK, true, true> : wf_shade_slots<BLOCK, false, true>)
+                 : (geo_lds ? wf_shade_slots<BLOCK, true, false> : wf_shade_slots<BLOCK, false, false>);
+}
 
 template <int LAY, int S, int BLOCK>
 hipError_t launch_extend(const KernelParams& kp, const WfParams& wf, int grid, size_t lds, hipStream_t st) {
-    auto kern = wf.sort ? (kp.lean ? wf_extend<LAY, S, BLOCK, false, true> : wf_extend<LAY, S, BLOCK, true, true>)
-                        : (kp.lean ? wf_extend<LAY, S, BLOCK, false, false>
-                                   : wf_extend<LAY, S, BLOCK, true, false>);
+    auto kern = kp.lean ? wf_extend<LAY, S, BLOCK, false> : wf_extend<LAY, S, BLOCK, true>;
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
@@ -1123,7 +1006,6 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams* wf_in, co
     const bool in_lds = wf_in_lds(kp.scene);
     kp.total_lanes = (uint32_t)total_lanes_for(img, cus);
     const uint32_t nseg = (uint32_t)wavefront_segments(kp.scene, cus);
-    const uint32_t per = in_lds ? 4u : 1u;                         // shade workgroups per segment
     // Several streams (ws.n > 1): batch i runs on stream i mod n, each stream
     // with its own queues/counters (wf_in[i]) and stack spill area, so one
     // batch's shade and the tail of its extend overlap another batch's extend.
@@ -1211,15 +1093,14 @@ hipError_t launch_wavefront(const KernelParams& kp_in, const WfParams* wf_in, co
                                                                             (size_t)MCPT_WF_GLOBAL_S * kGlobalBlock * 16 + 32,
                                                               bs);
                 if (e != hipSuccess) break;
-                if (wf.sort)
-                    hipLaunchKernelGGL(wf_shade, dim3(nseg * per), dim3(kShadeBlock), 0, bs, kb, wf, per);
-                else if (in_lds && ns == 1)   // alone on the GPU: 16 waves per segment keep HBM busy
-                    hipLaunchKernelGGL(shade_kernel<1024>(geo_bytes != 0), dim3(nseg), dim3(1024), geo_bytes, bs, kb, wf);
+                const bool sortb = wf.sort != 0;
+                if (in_lds && ns == 1)   // alone on the GPU: 16 waves per segment keep HBM busy
+                    hipLaunchKernelGGL(shade_kernel<1024>(geo_bytes != 0, sortb), dim3(nseg), dim3(1024), geo_bytes, bs, kb, wf);
                 else if (in_lds)              // beside an extend workgroup: 8 waves (2 x 80 VGPRs per SIMD)
-                    hipLaunchKernelGGL(shade_kernel<MCPT_WF_SHADE_LDS_BLOCK>(geo_bytes != 0), dim3(nseg),
+                    hipLaunchKernelGGL(shade_kernel<MCPT_WF_SHADE_LDS_BLOCK>(geo_bytes != 0, sortb), dim3(nseg),
                                        dim3(MCPT_WF_SHADE_LDS_BLOCK), geo_bytes, bs, kb, wf);
                 else
-                    hipLaunchKernelGGL(shade_kernel<256>(geo_bytes != 0), dim3(nseg), dim3(256), geo_bytes, bs, kb, wf);
+                    hipLaunchKernelGGL(shade_kernel<256>(geo_bytes != 0, sortb), dim3(nseg), dim3(256), geo_bytes, bs, kb, wf);
                 e = hipGetLastError();
             }
             if (e != hipSuccess) break;

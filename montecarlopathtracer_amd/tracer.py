@@ -180,7 +180,7 @@ class RenderParams:
     wf_batch: int = 0                 # wavefront paths per batch and stream, 0 = automatic (include/mcpt.h)
     mode: str = "cvmctracer"          # or "quinengine": rtx.hlsl path semantics (see for_quinengine)
     lean: bool = False                # kernels without traversal counters (same image; bench timing)
-    wf_sort: bool = False             # wavefront: material-sorted shade (class lists); same image
+    wf_sort: bool = False             # wavefront: shade sorts each block of slots by material; same image
     # scheduling (include/mcpt.h): never changes the image or the counters; 0 = automatic
     wf_streams: int = 0               # wavefront HIP streams (1..4)
     wf_refill: int = 0                # wavefront extend: ready lanes before a wave refills

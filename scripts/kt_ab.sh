@@ -15,7 +15,7 @@ for lib in $LIBS; do
 import csv, glob, sys
 f = glob.glob(sys.argv[1] + "/**/run_kernel_stats.csv", recursive=True)[0]
 for r in csv.DictReader(open(f)):
-    n = r["Name"].split("(")[0].replace("void mcpt::(anonymous namespace)::", "")
+    n = r["Name"]; n = n[n.find("wf_"):n.find("(mcpt::K")] if "wf_" in n else n[:40]
     print(f"  {float(r['TotalDurationNs'])/1e6:9.2f} ms {int(r['Calls']):5d} calls  {n}")
 PY
 done

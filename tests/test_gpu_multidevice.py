@@ -164,8 +164,8 @@ def test_plan_query_reports_the_schedule(mcpt, devices):
     assert 3 * 120 * (1 << 27) <= wf["wf_queue_bytes"] < 3 * 121 * (1 << 27) + (1 << 24)
     assert wf["wf_queue_bytes"] <= wf["workspace_bytes"] < wf["device_free_bytes"]
     assert wf["wf_batch_default"] == wf["wf_batch"]          # nothing shrunk on an empty device
-    srt = scene.plan(mcpt.RenderParams(pipeline="wavefront", wf_sort=True, **c2))
-    assert 3 * 160 * (1 << 27) <= srt["wf_queue_bytes"] < 3 * 161 * (1 << 27) + (1 << 24)
+    srt = scene.plan(mcpt.RenderParams(pipeline="wavefront", wf_sort=True, **c2))   # (sorts in LDS: same queues)
+    assert srt["wf_queue_bytes"] == wf["wf_queue_bytes"]
     mk = scene.plan(mcpt.RenderParams(**c2))
     assert mk["pipeline"] == 0 and mk["ready_thresh"] == 32 and mk["tail_units"] > 0 and mk["variant"] in (1, 2)
     o = scene.plan(mcpt.RenderParams(pipeline="wavefront", wf_streams=2, wf_refill=8, wf_batch=1 << 26, **c2))

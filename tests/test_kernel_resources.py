@@ -71,23 +71,24 @@ def test_shipped_kernels_fit_16_waves_per_cu(tmp_path):
     path = {k: v for k, v in kernels.items() if "path_kernel" in k}
     extend = {k: v for k, v in kernels.items() if "wf_extend" in k}
     assert len(path) == 18, sorted(path)  # 3 layouts x (DBG, QE, COUNT) variants
-    # 2 layouts x (lean, counting) x (queue order, sorted), + the wave-coherent bounce-0 extend (lean, counting)
-    assert len(extend) == 10, sorted(extend)
+    # 2 layouts x (lean, counting), + the wave-coherent bounce-0 extend (lean, counting)
+    assert len(extend) == 6, sorted(extend)
     for name, r in {**path, **extend}.items():
         assert r["vgpr"] + r["agpr"] <= 128, (name, r)
         # product variants: the DBG unit-counter megakernels (template arg 4 true) may spill
         if "wf_extend" in name or re.search(r"path_kernelILb[01]ELi\d+ELi\d+ELb0E", name):
             assert r["scratch"] == 0, (name, r)
     # the residency the wavefront's schedule is built on: the
-    # lean queue-order extend of global-memory scenes (template <LAY 0, S, 256,
-    # lean, queue order>) at <= 80 VGPRs -- six workgroups per CU -- and the LDS
+    # lean extend of global-memory scenes (template <LAY 0, S, 256, lean>) at
+    # <= 80 VGPRs -- six workgroups per CU -- and the LDS
     # scenes' (LAY 1) at <= 88 beside two <= 80-VGPR shade waves per SIMD
-    g_lean = [r for k, r in extend.items() if re.search(r"wf_extendILi0ELi\d+ELi256ELb0ELb0E", k)]
-    l_lean = [r for k, r in extend.items() if re.search(r"wf_extendILi1ELi4ELi1024ELb0ELb0E", k)]
+    g_lean = [r for k, r in extend.items() if re.search(r"wf_extendILi0ELi\d+ELi256ELb0EE", k)]
+    l_lean = [r for k, r in extend.items() if re.search(r"wf_extendILi1ELi4ELi1024ELb0EE", k)]
     assert len(g_lean) == 1 and len(l_lean) == 1, sorted(extend)
     assert g_lean[0]["vgpr"] <= 80 and l_lean[0]["vgpr"] <= 88, (g_lean, l_lean)
+    # (both shades: queue order and the material sort)
     shade = [r for k, r in kernels.items() if re.search(r"wf_shade_slotsILi512E", k)]
-    assert shade and all(r["vgpr"] <= 80 for r in shade), shade
+    assert len(shade) == 4 and all(r["vgpr"] <= 80 for r in shade), shade
     # the other wavefront kernels run at most 512 VGPRs' worth of waves; keep them spill-free
     for name, r in kernels.items():
         if "wf_" in name:
@@ -153,7 +154,7 @@ def test_codegen_flags_still_do_their_job(tmp_path):
     assert extends
     for n in extends:
         assert any(x.startswith("s_setprio 3") for x in k[n]), n
-    g_ext = one(r"wf_extendILi0ELi\d+ELi256ELb0ELb0E")       # global layout, lean, queue order
+    g_ext = one(r"wf_extendILi0ELi\d+ELi256ELb0EE")       # global layout, lean
     mk_glob = one(r"path_kernelILb0ELi8ELi256ELb0ELb1ELb0E")   # global layout, lean megakernel
     mk_lds = one(r"path_kernelILb1ELi4ELi1024ELb0ELb0ELb0E")   # LDS layout, lean megakernel
     cap = 5                                                     # MCPT_DESCENT_CAP_GLOBAL
