@@ -812,10 +812,10 @@ wf_shade_slots(const KernelParams kp, const WfParams wf) {
             if (i < total) {
                 const size_t js = seg0 + i;
                 const int32_t htri = reinterpret_cast<const int32_t*>(qb + qf(0, kQHIT, qs))[js];
-                const uint32_t depth = imp ? 0u : __float_as_uint(qb[qf(js, kQD, qs)].w);
+                // (every ray of queue b is at depth b; an empty slot is a miss)
                 const int32_t lim = qe ? 3 * kp.max_depth : kp.max_depth;
                 k = kClassTerminate;
-                if (htri >= 0 && depth != kNoRay && (int32_t)depth < lim) {
+                if (htri >= 0 && wf.bounce < lim) {
                     const GpuGeom& gm = geoms[__float_as_uint(tris[htri + 1].w)];
                     if (!is_emitter(gm)) k = material_class(gm);
                 }
