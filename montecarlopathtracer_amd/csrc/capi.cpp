@@ -353,7 +353,7 @@ void build_image(mcpt_scene& s, bool force_global) {
     }
     const size_t off_tris = 0;
     if (total > 0xFFFFFFF0u) throw mcpt::Error{MCPT_E_UNSUPPORTED, "scene image exceeds 4 GiB"};
-    if (ord.n_slots >= (1u << 30) || nl >= (1u << 30)) throw mcpt::Error{MCPT_E_UNSUPPORTED, "KD tree too large"};
+    if (ord.n_slots >= (1u << 29) || nl >= (1u << 30)) throw mcpt::Error{MCPT_E_UNSUPPORTED, "KD tree too large"};
     s.image.assign(total, 0);
     s.tri_order = ord.tri_order;
     unsigned char* img = s.image.data();
@@ -386,7 +386,11 @@ void build_image(mcpt_scene& s, bool force_global) {
         const mcpt::KdNode& n = hs.nodes[i];
         uint32_t w[2];
         if (n.axis) {
-            w[0] = ((n.axis - 1u) << 30) | ord.node_new[n.left];
+            // LDS layout: the left child's device node index (its 8-B record
+            // pair at slot index + 1); global layout: the 16-B offset 3m of the
+            // children's 48-B pair record m (no index arithmetic per step)
+            const uint32_t dl = ord.node_new[n.left];
+            w[0] = ((n.axis - 1u) << 30) | (boxes ? 3u * ((dl - 1u) / 2u) : dl);
             std::memcpy(&w[1], &n.split, 4);
         } else {
             w[0] = (3u << 30) | leaf_begin_new[i];

@@ -52,6 +52,18 @@ __device__ __forceinline__ float min_qnan(float a, float b) {
     asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
     return r;
 }
+// the same over three operands in one instruction (v_max3 / v_min3: the
+// nested maxNum / minNum, so the same quiet-NaN rule)
+__device__ __forceinline__ float max3_qnan(float a, float b, float c) {
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ float min3_qnan(float a, float b, float c) {
+    float r;
+    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
 __device__ __forceinline__ float sel3(int a, float x, float y, float z) {
     return a == 0 ? x : (a == 1 ? y : z);
 }
@@ -311,7 +323,6 @@ __device__ __forceinline__ float h2f(uint32_t bits16) {
 // PERFLOG round 6.)  Equal decisions for every box with lo <= hi; an
 // inverted (empty-node) box is always culled.
 __device__ __forceinline__ bool box_hit(const RayState& r, uint32_t b0, uint32_t b1, uint32_t b2) {
-    float lo = 0.0f, hi = r.best;
     const float lx = h2f(b0 & 0xFFFFu), hx = h2f(b1 >> 16);
     const float ly = h2f(b0 >> 16), hy = h2f(b2 & 0xFFFFu);
     const float lz = h2f(b1 & 0xFFFFu), hz = h2f(b2 >> 16);
@@ -319,8 +330,8 @@ __device__ __forceinline__ bool box_hit(const RayState& r, uint32_t b0, uint32_t
     const float tx0 = ((nx ? hx : lx) - r.o.x) * r.ix, tx1 = ((nx ? lx : hx) - r.o.x) * r.ix;
     const float ty0 = ((ny ? hy : ly) - r.o.y) * r.iy, ty1 = ((ny ? ly : hy) - r.o.y) * r.iy;
     const float tz0 = ((nz ? hz : lz) - r.o.z) * r.iz, tz1 = ((nz ? lz : hz) - r.o.z) * r.iz;
-    lo = max_qnan(max_qnan(max_qnan(lo, tx0), ty0), tz0);
-    hi = min_qnan(min_qnan(min_qnan(hi, tx1), ty1), tz1);
+    const float lo = max_qnan(max3_qnan(0.0f, tx0, ty0), tz0);
+    const float hi = min_qnan(min3_qnan(r.best, tx1, ty1), tz1);
     return !(lo * kEpsLo > hi * kEpsHi);
 }
 
@@ -397,7 +408,7 @@ __device__ __forceinline__ int descend_steps(RayState& r, const uint2* __restric
         const uint32_t left = w0 & kLeftMask;
         uint4 pr, bx0, bx1;
         if constexpr (BOXES) {            // 48-B pair record: words, box(left), box(right)
-            const uint4* rec = pairs + 3u * ((left - 1u) >> 1);
+            const uint4* rec = pairs + left;   // (global layout: left = the record's 16-B offset)
             pr = rec[0];
             bx0 = rec[1];
             bx1 = rec[2];
