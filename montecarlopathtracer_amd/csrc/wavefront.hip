@@ -239,8 +239,11 @@ __global__ void __launch_bounds__(kGenBlock) wf_generate(const KernelParams kp, 
 #ifndef MCPT_WF_DESCENT_CAP
 #define MCPT_WF_DESCENT_CAP 5
 #endif
+// Global-memory scenes: 6 since round 6's cheaper descent step (C4 cap
+// 4 / 5 / 6 / 7: 10.84 / 11.19 / 11.40 / 11.06 and 10.86 / 11.14 / 11.30 /
+// 11.05 G rays/s, PERFLOG row 164); the megakernel keeps MCPT_DESCENT_CAP_GLOBAL
 #ifndef MCPT_WF_DESCENT_CAP_GLOBAL
-#define MCPT_WF_DESCENT_CAP_GLOBAL MCPT_DESCENT_CAP_GLOBAL
+#define MCPT_WF_DESCENT_CAP_GLOBAL 6
 #endif
 constexpr int kWfLdsCap = MCPT_WF_DESCENT_CAP;
 

@@ -123,7 +123,8 @@ def test_codegen_flags_still_do_their_job(tmp_path):
       only uses priorities 0 and 1): 1 / 0;
     * -unroll-threshold=2000 (wavefront.hip, render.hip): the global-memory
       variants' capped descent unrolled -- 12 fp16 box-bound conversions per
-      step (two child boxes), so 12 x cap of them: 60 / 12;
+      step (two child boxes), so 12 x cap of them (caps 6 / 5: 72 and 60,
+      one step's 12 without the option);
     * -two-entry-phi-node-folding-threshold=8 (wavefront.hip): if-diamonds of
       the global extend folded into selects -- exec-mask regions
       (`s_and_saveexec_b64`) in the lean queue-order global extend: 83 / 103;
@@ -157,9 +158,8 @@ def test_codegen_flags_still_do_their_job(tmp_path):
     g_ext = one(r"wf_extendILi0ELi\d+ELi256ELb0EE")       # global layout, lean
     mk_glob = one(r"path_kernelILb0ELi8ELi256ELb0ELb1ELb0E")   # global layout, lean megakernel
     mk_lds = one(r"path_kernelILb1ELi4ELi1024ELb0ELb0ELb0E")   # LDS layout, lean megakernel
-    cap = 5                                                     # MCPT_DESCENT_CAP_GLOBAL
-    assert count(g_ext, "v_cvt_f32_f16") >= 12 * cap
-    assert count(mk_glob, "v_cvt_f32_f16") >= 12 * cap
+    assert count(g_ext, "v_cvt_f32_f16") >= 12 * 6               # MCPT_WF_DESCENT_CAP_GLOBAL
+    assert count(mk_glob, "v_cvt_f32_f16") >= 12 * 5             # MCPT_DESCENT_CAP_GLOBAL
     assert count(g_ext, "s_and_saveexec_b64") <= 93
     assert count(mk_lds, "v_mul_f32_e32") <= 182 and count(mk_glob, "v_mul_f32_e32") <= 279
     prim = one(r"wf_extend_primaryILi4ELi1024ELb0E")
